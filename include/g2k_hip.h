@@ -1,0 +1,171 @@
+/*
+ * g2k_hip.h — C ABI of libg2k_hip.so, the MI355X (gfx950) implementation of the
+ * g2k_lstm_mcr per-frame path of serenetech90/multimodaltraj_2.
+ *
+ * The reference has no native plugin API: its boundary is the Python class
+ * `g2k_lstm_mcr` plus the TF session feed/fetch protocol.
+ * Each entry point below replaces one piece of that boundary; the replaced
+ * reference interface is cited per function.  The Python mirror classes in
+ * multimodaltraj_2_amd/ bind these through ctypes.
+ *
+ * Conventions (all entry points):
+ *   - every buffer is caller-owned DEVICE memory, contiguous, row-major fp32
+ *     unless stated; nullable pointers are marked "or NULL";
+ *   - launches are asynchronous on `stream` (a hipStream_t; NULL = default);
+ *     no allocation, no host synchronisation: capturable into a hipGraph;
+ *   - return 0 on success, a negative G2K_E* code on failure; the message of
+ *     the last failure on this thread is in g2k_last_error();
+ *   - deterministic: fixed reduction order, no float atomics;
+ *   - fixed model geometry: T (obs_len) = 8, L (pred_len) = 12, D = 16
+ *     (= neighborhood_size / grid_size, train.py:93); H a multiple of 64 in
+ *     [64, 512]; Nmax in [1, 256].
+ */
+#ifndef G2K_HIP_H
+#define G2K_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define G2K_ABI_VERSION 1
+
+enum {
+  G2K_OK = 0,
+  G2K_EINVAL = -1,     /* bad dims / null required pointer */
+  G2K_ELAUNCH = -2,    /* HIP launch error */
+  G2K_ELDS = -3,       /* requested geometry exceeds LDS */
+  G2K_EUNSUPPORTED = -4
+};
+
+/* Geometry of one launch (validated on entry). */
+typedef struct g2k_dims {
+  int32_t S;       /* scenes (batches) in this launch                         */
+  int32_t F;       /* frames per scene (max; see n_frames)                    */
+  int32_t T;       /* obs_len, must be 8        (argParser.py:26-28)          */
+  int32_t L;       /* pred_len, must be 12      (models/g2k_lstm_mcr.py:124)  */
+  int32_t D;       /* hidden_len, must be 16    (train.py:93)                 */
+  int32_t H;       /* rnn_size                  (argParser.py:8-9)            */
+  int32_t Nmax;    /* padded pedestrians per scene                            */
+  int32_t W;       /* position rows per scene, >= (F-1)*stride + T            */
+  int32_t stride;  /* position-window advance per frame (1 sliding, 0 fixed)  */
+} g2k_dims;
+
+/* Model parameters (device pointers). Shapes as in the reference. */
+typedef struct g2k_weights {
+  const float* Wi;   /* [Nmax, D]  weight_input/weight_i   train.py:168-171     */
+  const float* Wii;  /* [D, T]     weight_input/weight_ii  train.py:172-175     */
+  const float* Wv;   /* [T, D+2]   krnl_weights/weight_v   g2k_lstm_mcr.py:49   */
+  const float* bv;   /* [D]        krnl_weights/bias_v     g2k_lstm_mcr.py:55   */
+  const float* Wr;   /* [T, 2]     krnl_embed/weight_r     g2k_lstm_mcr.py:72   */
+  const float* Wc;   /* [2L, T]    krnl_weights/weight_c   g2k_lstm_mcr.py:65   */
+  const float* Wo;   /* [T, Nmax]  krnl_weights/weight_o   g2k_lstm_mcr.py:61   */
+} g2k_weights;
+
+int g2k_abi_version(void);
+const char* g2k_last_error(void);
+
+/* Bytes of dynamic LDS per g2k_frames_kernel workgroup for `d` (0 if unsupported). */
+int64_t g2k_step_lds_bytes(const g2k_dims* d);
+
+/* Bytes of caller-provided device workspace g2k_step_fused_f32 needs for `d`
+ * (attention weights [S, F, D, D] + per-chunk ADE/FDE partial sums); -1 on
+ * invalid dims.  The workspace must be 16-byte aligned. */
+int64_t g2k_step_workspace_bytes(const g2k_dims* d);
+
+/*
+ * g2k_step_fused_f32 — the whole per-frame body of train.py:197-276 for S
+ * scenes x F frames, one launch:
+ *   a2 window norms (train.py:76-85 arithmetic; window = rows f*stride + t),
+ *   a3 X0 = Wii @ (Bv @ Wi) (train.py:178-180),
+ *   a4 Ve = vislet @ Wi, Rel = Ve*Ve (train.py:182-195),
+ *   a7 g2k_lstm_mcr.forward (models/g2k_lstm_mcr.py:99-124),
+ *   a8 attention + hidden recurrence (train.py:240-252),
+ *   a9 validation ADE/FDE sums (train.py:640-674).
+ * Replaces: the frame loop train.py:197-276 (four sess.run + ~13 .eval() per
+ * frame) and its per-batch setup train.py:178-195.
+ * Two stream-ordered launches: a frame-parallel kernel (a2-a7, a9) and the
+ * frame-sequential recurrence kernel (a8); `workspace` carries the attention
+ * weights between them (g2k_step_workspace_bytes).
+ *
+ *   pos      [S, W, Nmax, 2]       pedestrian (x, y) rows
+ *   vislet   [S, 2, Nmax]          load_traj.py:139 rows 4:6 slice
+ *   G        [S, D, T]             `_2dconv_in` feed (train.py:158, 232)
+ *   targets  [S, F, Nmax, L, 2]    target assigned to each prediction row
+ *   n_active [S] int32             pedestrians present (<= Nmax)
+ *   n_frames [S] int32 or NULL     frames present (<= F); NULL = F
+ *   ped_mask [S, Nmax] uint8 or NULL  rows with a target; NULL = all active
+ *   h_in     [S, D, H]             hidden_state entering frame 0
+ *   h_out    [S, D, H]             hidden_state after the last frame (may alias h_in)
+ *   pred     [S, F, 2L, Nmax]      pred_path_band per frame (rows x then y)
+ *   metrics  [S, 8]                {sum ade_spec, count, sum |fde|^2,
+ *                                   sum ade_l2, sum |fde|, frames, 0, 0}
+ *   A_out    [S, F, D, D] or NULL  krnl_mdl.attn per frame (frames < n_frames)
+ *   cost_out [S, F, T, T] or NULL  krnl_mdl.cost per frame (frames < n_frames)
+ *   lambda                          lambda_param (argParser.py, 5e-4)
+ *   workspace, workspace_bytes      >= g2k_step_workspace_bytes(d)
+ * h_out must not alias h_in across scenes being read (same-scene aliasing is fine).
+ */
+int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w,
+                       const float* pos, const float* vislet, const float* G,
+                       const float* targets, const int32_t* n_active,
+                       const int32_t* n_frames, const uint8_t* ped_mask,
+                       const float* h_in, float* h_out, float* pred,
+                       float* metrics, float* A_out, float* cost_out,
+                       float lambda, void* workspace, int64_t workspace_bytes,
+                       void* stream);
+
+/*
+ * g2k_mcr_forward_f32 — g2k_lstm_mcr.forward() for S independent feeds.
+ * Replaces: models/g2k_lstm_mcr.py:99-124 and the sess.run at
+ * train.py:226-238 (fetches pred_path_band, cost; attn read at :240).
+ *   X    [S, D+2, D]  (`outputs` feed)    Rel [S, 2, D] (`rel_features`)
+ *   G    [S, D, T]    (`ngh` feed)        n_active [S] int32 (`out_size`)
+ *   A_out [S, D, D]   cost_out [S, T, T]  pred [S, 2L, Nmax]
+ * Only d->S, T, L, D, Nmax are read.
+ */
+int g2k_mcr_forward_f32(const g2k_dims* d, const g2k_weights* w,
+                        const float* X, const float* Rel, const float* G,
+                        const int32_t* n_active, float* A_out, float* cost_out,
+                        float* pred, float lambda, void* stream);
+
+/*
+ * g2k_frame_recurrence_f32 — attention + hidden-state recurrence of
+ * train.py:240-252 over `frames` consecutive attention matrices.
+ * Replaces: train.py:240-252 (and its copy at 622-634).
+ *   A [S, frames, D, D] (16-byte aligned); h [S, D, H] updated in place.
+ *   Reads d->S, D, H.
+ */
+int g2k_frame_recurrence_f32(const g2k_dims* d, const float* A, float* h,
+                             int32_t frames, void* stream);
+
+/*
+ * g2k_ade_fde_f32 — displacement errors from predictions.
+ *   variant 0: validation sums (train.py:640-674) -> out [S, 8] as metrics above
+ *   variant 1: get_mean_error (sample.py:21-82) -> out [S, 8] =
+ *              {ADE, FDE, counter, 0...}; pred/targets are [S, 2L, Nmax] /
+ *              [S, Nmax, L, 2] with F = 1 and obs_length = d->T.
+ * Replaces: the numpy error loops train.py:636-674 and sample.py:21-82.
+ *   pred [S, F, 2L, Nmax]; targets [S, F, Nmax, L, 2]; n_active [S];
+ *   n_frames [S] or NULL; ped_mask [S, Nmax] or NULL.
+ */
+int g2k_ade_fde_f32(const g2k_dims* d, const float* pred, const float* targets,
+                    const int32_t* n_active, const int32_t* n_frames,
+                    const uint8_t* ped_mask, int32_t variant, float* out,
+                    void* stream);
+
+/*
+ * Elementwise relation ops of nri_learned.py over [rows, cols] matrices.
+ * g2k_infer_rlns_f32:  out = sigmoid(adj)           (nri_learned.py:16-21)
+ * g2k_eval_rln_ngh_f32: out = softmax(adj, axis=-1) (nri_learned.py:23-28)
+ */
+int g2k_infer_rlns_f32(const float* adj, float* out, int64_t rows, int32_t cols,
+                       void* stream);
+int g2k_eval_rln_ngh_f32(const float* adj, float* out, int64_t rows,
+                         int32_t cols, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* G2K_HIP_H */

@@ -1,0 +1,272 @@
+"""Host API of the fused per-frame step (train.py:197-276) over device tensors.
+
+Everything here is plumbing around the C ABI (include/g2k_hip.h): it checks
+shapes/dtypes/devices on the host, allocates outputs with torch, and calls
+``g2k_step_fused_f32`` / ``g2k_mcr_forward_f32`` / ``g2k_frame_recurrence_f32``
+/ ``g2k_ade_fde_f32`` on the current HIP stream.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, fields
+
+import numpy as np
+import torch
+
+from . import _lib
+
+OBS_LEN = 8          # argParser.py:26-28
+PRED_LEN = 12        # models/g2k_lstm_mcr.py:124 hard-codes 12
+HIDDEN_LEN = 16      # neighborhood_size / grid_size = 64 / 4 (train.py:93)
+LAMBDA = 5e-4        # argParser.py --lambda_param
+METRIC_FIELDS = ("ade_spec_sum", "count", "fde_sq_sum", "ade_l2_sum", "fde_l2_sum",
+                 "frames", "reserved0", "reserved1")
+
+
+@dataclass
+class G2KParams:
+    """Model parameters, shapes as in the reference (padded to Nmax where the
+    reference sizes them by the batch's num_nodes)."""
+    Wi: torch.Tensor    # [Nmax, D]   train.py:168-171
+    Wii: torch.Tensor   # [D, T]      train.py:172-175
+    Wv: torch.Tensor    # [T, D+2]    models/g2k_lstm_mcr.py:49-53
+    bv: torch.Tensor    # [D]         models/g2k_lstm_mcr.py:55-59
+    Wr: torch.Tensor    # [T, 2]      models/g2k_lstm_mcr.py:72-76
+    Wc: torch.Tensor    # [2L, T]     models/g2k_lstm_mcr.py:65-69
+    Wo: torch.Tensor    # [T, Nmax]   models/g2k_lstm_mcr.py:61-64
+
+    @property
+    def nmax(self) -> int:
+        return int(self.Wi.shape[0])
+
+    def to(self, device) -> "G2KParams":
+        return G2KParams(**{f.name: getattr(self, f.name).to(device) for f in fields(self)})
+
+    def numpy(self) -> dict:
+        return {f.name: getattr(self, f.name).detach().cpu().numpy() for f in fields(self)}
+
+    def check(self, device):
+        D, T, L2 = HIDDEN_LEN, OBS_LEN, 2 * PRED_LEN
+        n = self.nmax
+        want = dict(Wi=(n, D), Wii=(D, T), Wv=(T, D + 2), bv=(D,), Wr=(T, 2), Wc=(L2, T),
+                    Wo=(T, n))
+        for k, shp in want.items():
+            t = getattr(self, k)
+            if tuple(t.shape) != shp:
+                raise ValueError(f"param {k}: shape {tuple(t.shape)}, expected {shp}")
+            _check_dev(k, t, device, torch.float32)
+
+    def abi(self) -> _lib.G2KWeights:
+        return _lib.G2KWeights(*(getattr(self, f.name).data_ptr() for f in fields(self)))
+
+
+def init_params(nmax: int, seed: int = 0, device="cpu") -> G2KParams:
+    """~N(0, 1) weights (init_w stddev 1, train.py:116-117 /
+    models/g2k_lstm_mcr.py:10), generated on the host with a seeded NumPy
+    Generator so the oracle sees the same values."""
+    rng = np.random.default_rng(seed)
+    D, T, L2 = HIDDEN_LEN, OBS_LEN, 2 * PRED_LEN
+    shapes = [("Wi", (nmax, D)), ("Wii", (D, T)), ("Wv", (T, D + 2)), ("bv", (D,)),
+              ("Wr", (T, 2)), ("Wc", (L2, T)), ("Wo", (T, nmax))]
+    return G2KParams(**{k: torch.from_numpy(rng.standard_normal(s).astype(np.float32)).to(device)
+                        for k, s in shapes})
+
+
+def _check_dev(name, t, device, dtype):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+@dataclass
+class StepOutputs:
+    pred: torch.Tensor       # [S, F, 2L, Nmax]
+    h: torch.Tensor          # [S, D, H]
+    metrics: torch.Tensor    # [S, 8]
+    attn: torch.Tensor | None = None   # [S, F, D, D]
+    cost: torch.Tensor | None = None   # [S, F, T, T]
+
+
+def step_lds_bytes(S, F, H, Nmax, W, stride) -> int:
+    lib = _lib.load()
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride)
+    return int(lib.g2k_step_lds_bytes(ctypes.byref(d)))
+
+
+def step_workspace_bytes(S, F, H, Nmax, W, stride) -> int:
+    lib = _lib.load()
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride)
+    return int(lib.g2k_step_workspace_bytes(ctypes.byref(d)))
+
+
+_WS = {}
+
+
+def _workspace(nbytes, device):
+    """Per-device reusable workspace (grown on demand, allocated outside any
+    timed region after the first call)."""
+    key = (device.type, device.index)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def step_fused(params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
+               ped_mask=None, stride=1, lam=LAMBDA, out: StepOutputs | None = None,
+               want_attn=False, stream=None, h_out=None) -> StepOutputs:
+    """One pass of the per-frame body of train.py:197-276 over S scenes.
+
+    pos [S, W, Nmax, 2], vislet [S, 2, Nmax], G [S, D, T],
+    targets [S, F, Nmax, L, 2], n_active [S] int32, h [S, D, H].
+    ``F`` is taken from ``targets``.  Returns pred/h/metrics (and per-frame
+    attn / cost when ``want_attn``)."""
+    lib = _lib.load()
+    dev = pos.device
+    if dev.type != "cuda":
+        raise ValueError("step_fused runs on the GPU only (no CPU fallback)")
+    S, W, Nmax, two = pos.shape
+    if two != 2:
+        raise ValueError(f"pos: last dim {two}, expected 2")
+    F = int(targets.shape[1])
+    H = int(h.shape[2])
+    params.check(dev)
+    if params.nmax != Nmax:
+        raise ValueError(f"params Nmax={params.nmax} but pos Nmax={Nmax}")
+    exp = dict(pos=(S, W, Nmax, 2), vislet=(S, 2, Nmax), G=(S, HIDDEN_LEN, OBS_LEN),
+               targets=(S, F, Nmax, PRED_LEN, 2), h=(S, HIDDEN_LEN, H))
+    for k, t in dict(pos=pos, vislet=vislet, G=G, targets=targets, h=h).items():
+        if tuple(t.shape) != exp[k]:
+            raise ValueError(f"{k}: shape {tuple(t.shape)}, expected {exp[k]}")
+        _check_dev(k, t, dev, torch.float32)
+    if tuple(n_active.shape) != (S,):
+        raise ValueError("n_active must be [S]")
+    _check_dev("n_active", n_active, dev, torch.int32)
+    if n_frames is not None:
+        _check_dev("n_frames", n_frames, dev, torch.int32)
+    if ped_mask is not None:
+        _check_dev("ped_mask", ped_mask, dev, torch.uint8)
+        if tuple(ped_mask.shape) != (S, Nmax):
+            raise ValueError("ped_mask must be [S, Nmax]")
+    if out is None:
+        out = StepOutputs(
+            pred=torch.empty((S, F, 2 * PRED_LEN, Nmax), device=dev, dtype=torch.float32),
+            h=h_out if h_out is not None else torch.empty_like(h),
+            metrics=torch.empty((S, 8), device=dev, dtype=torch.float32),
+            attn=(torch.empty((S, F, HIDDEN_LEN, HIDDEN_LEN), device=dev, dtype=torch.float32)
+                  if want_attn else None),
+            cost=(torch.empty((S, F, OBS_LEN, OBS_LEN), device=dev, dtype=torch.float32)
+                  if want_attn else None))
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride)
+    w = params.abi()
+    nws = int(lib.g2k_step_workspace_bytes(ctypes.byref(d)))
+    if nws < 0:
+        _lib.check("g2k_step_workspace_bytes", -1)
+    ws = _workspace(nws, dev)
+    rc = lib.g2k_step_fused_f32(ctypes.byref(d), ctypes.byref(w), _ptr(pos), _ptr(vislet),
+                                _ptr(G), _ptr(targets), _ptr(n_active), _ptr(n_frames),
+                                _ptr(ped_mask), _ptr(h), _ptr(out.h), _ptr(out.pred),
+                                _ptr(out.metrics), _ptr(out.attn), _ptr(out.cost),
+                                float(lam), ws.data_ptr(), nws, _stream(stream))
+    _lib.check("g2k_step_fused_f32", rc)
+    return out
+
+
+def mcr_forward(params: G2KParams, X, Rel, G, n_active, *, lam=LAMBDA, stream=None):
+    """g2k_lstm_mcr.forward() for S feeds (models/g2k_lstm_mcr.py:99-124).
+    X [S, D+2, D], Rel [S, 2, D], G [S, D, T] -> (attn [S,D,D], cost [S,T,T],
+    pred [S, 2L, Nmax])."""
+    lib = _lib.load()
+    dev = X.device
+    S = int(X.shape[0])
+    Nmax = int(params.Wo.shape[1])
+    for k, t, shp in (("X", X, (S, HIDDEN_LEN + 2, HIDDEN_LEN)), ("Rel", Rel, (S, 2, HIDDEN_LEN)),
+                      ("G", G, (S, HIDDEN_LEN, OBS_LEN))):
+        if tuple(t.shape) != shp:
+            raise ValueError(f"{k}: shape {tuple(t.shape)}, expected {shp}")
+        _check_dev(k, t, dev, torch.float32)
+    _check_dev("n_active", n_active, dev, torch.int32)
+    for k in ("Wv", "bv", "Wr", "Wc", "Wo"):
+        _check_dev(k, getattr(params, k), dev, torch.float32)
+    attn = torch.empty((S, HIDDEN_LEN, HIDDEN_LEN), device=dev, dtype=torch.float32)
+    cost = torch.empty((S, OBS_LEN, OBS_LEN), device=dev, dtype=torch.float32)
+    pred = torch.empty((S, 2 * PRED_LEN, Nmax), device=dev, dtype=torch.float32)
+    d = _lib.G2KDims(S, 1, OBS_LEN, PRED_LEN, HIDDEN_LEN, 64, Nmax, OBS_LEN, 0)
+    w = _lib.G2KWeights(None, None, params.Wv.data_ptr(), params.bv.data_ptr(),
+                        params.Wr.data_ptr(), params.Wc.data_ptr(), params.Wo.data_ptr())
+    rc = lib.g2k_mcr_forward_f32(ctypes.byref(d), ctypes.byref(w), _ptr(X), _ptr(Rel), _ptr(G),
+                                 _ptr(n_active), _ptr(attn), _ptr(cost), _ptr(pred), float(lam),
+                                 _stream(stream))
+    _lib.check("g2k_mcr_forward_f32", rc)
+    return attn, cost, pred
+
+
+def frame_recurrence(A, h, *, stream=None):
+    """train.py:240-252 over F attention matrices: A [S, F, D, D], h [S, D, H]
+    (updated in place and returned)."""
+    lib = _lib.load()
+    S, F = int(A.shape[0]), int(A.shape[1])
+    H = int(h.shape[2])
+    _check_dev("A", A, A.device, torch.float32)
+    _check_dev("h", h, A.device, torch.float32)
+    if tuple(A.shape[2:]) != (HIDDEN_LEN, HIDDEN_LEN) or tuple(h.shape) != (S, HIDDEN_LEN, H):
+        raise ValueError("A must be [S, F, 16, 16] and h [S, 16, H]")
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, 1, OBS_LEN, 0)
+    rc = lib.g2k_frame_recurrence_f32(ctypes.byref(d), _ptr(A), _ptr(h), F, _stream(stream))
+    _lib.check("g2k_frame_recurrence_f32", rc)
+    return h
+
+
+def ade_fde(pred, targets, n_active, *, n_frames=None, ped_mask=None, variant=0,
+            obs_length=OBS_LEN, stream=None):
+    """Error sums from predictions.  variant 0: train.py:640-674 sums
+    (pred [S, F, 2L, Nmax], targets [S, F, Nmax, L, 2]); variant 1:
+    sample.py get_mean_error (pred [S, 2L, Nmax], targets [S, Nmax, L, 2]).
+    Returns [S, 8]."""
+    lib = _lib.load()
+    dev = pred.device
+    if variant == 0:
+        S, F, _, Nmax = pred.shape
+    else:
+        S, _, Nmax = pred.shape
+        F = 1
+    out = torch.empty((S, 8), device=dev, dtype=torch.float32)
+    T = OBS_LEN if variant == 0 else obs_length
+    d = _lib.G2KDims(S, F, T, PRED_LEN, HIDDEN_LEN, 64, Nmax, OBS_LEN, 0)
+    if variant == 1:
+        # the kernel reads obs_length from d.T; geometry checks need T=8, so
+        # only the default observed length is accepted here
+        if obs_length != OBS_LEN:
+            raise ValueError("get_mean_error variant supports observed_length=8 only")
+    for k, t in (("pred", pred), ("targets", targets)):
+        _check_dev(k, t, dev, torch.float32)
+    rc = lib.g2k_ade_fde_f32(ctypes.byref(d), _ptr(pred), _ptr(targets), _ptr(n_active),
+                             _ptr(n_frames), _ptr(ped_mask), int(variant), _ptr(out),
+                             _stream(stream))
+    _lib.check("g2k_ade_fde_f32", rc)
+    return out
+
+
+def batch_errors(metrics: torch.Tensor, leave_dataset=None, num_nodes=None):
+    """train.py:668-674 per-batch reduction of the metric sums -> (ADE_b, FDE_b)
+    per scene, on the host."""
+    m = metrics.detach().double().cpu().numpy()
+    ade = np.where(m[:, 1] > 0, m[:, 0] / np.maximum(m[:, 1], 1), np.nan)
+    denom = np.asarray(num_nodes, dtype=np.float64) if leave_dataset == 5 else m[:, 5]
+    fde = np.where(m[:, 1] > 0, np.sqrt(m[:, 2]) / np.maximum(denom, 1), np.nan)
+    return ade, fde

@@ -1,0 +1,32 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C ABI)")
+
+
+def close(got, ref, tol=1e-4):
+    """SURVEY.md finding 7 / §8(d): |got - ref| <= tol * max(1, |ref|)."""
+    import numpy as np
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
+    return float(err.max()) if err.size else 0.0
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from multimodaltraj_2_amd import _lib
+    _lib.load()   # fails loudly if the HIP library is missing
+    return torch.device("cuda:0")
