@@ -20,6 +20,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "g2k_hip.h"
 
@@ -32,7 +33,6 @@ constexpr int kD = 16;    // hidden_len
 constexpr int kNT = 256;  // threads per workgroup
 constexpr int kMaxN = 256;
 constexpr int kRecurChunk = 32;         // As tiles resident in LDS in g2k_recur_kernel
-constexpr int kFramesLdsBudget = 48 * 1024;
 
 thread_local char g_err[512] = "";
 
@@ -65,7 +65,29 @@ __device__ unsigned long long g2k_stamps[64];
 #define STAMP(k) do {} while (0)
 #endif
 
+#ifdef G2K_STAMPS_RECUR
+// diagnostic build only: in-frame stamps of wave 0 of workgroup 0, frame 5
+__device__ unsigned long long g2k_rstamps[16];
+__device__ int g2k_rframe;
+#define RSTAMP(k)                                                             \
+  do {                                                                        \
+    unsigned long long _t;                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && g2k_rframe == 5) g2k_rstamps[(k)] = _t; \
+  } while (0)
+#else
+#define RSTAMP(k) do {} while (0)
+#endif
+
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// Diagnostic ablation switches for tools/ablate_recur.py (never set in the
+// shipped build; every switch breaks the results on purpose).
+#ifndef G2K_ABL
+#define G2K_ABL 0
+#endif
 
 // LDS-DMA: 16 bytes per lane, LDS destination = wave-uniform base + 16*lane.
 __device__ __forceinline__ void dma16(const float* gsrc, float* lds_wave_base) {
@@ -74,11 +96,22 @@ __device__ __forceinline__ void dma16(const float* gsrc, float* lds_wave_base) {
                                    0);
 }
 
-// Copy n4 float4s (contiguous, 16-B aligned) global -> LDS with the whole
-// workgroup; the caller waits (vmcnt(0)) and barriers before reading.
-__device__ __forceinline__ void dma_copy(const float* g, float* lds, int n4, int wv, int lane) {
-  for (int i = wv * 64; i < n4; i += kNT) {
+// Copy n4 float4s (contiguous, 16-B aligned) global -> LDS with a workgroup
+// of NT threads; the caller waits (vmcnt(0)) and barriers before reading.
+template <int NT>
+__device__ __forceinline__ void dma_copy_n(const float* g, float* lds, int n4, int wv, int lane) {
+  for (int i = wv * 64; i < n4; i += NT) {
     if (i + lane < n4) dma16(g + (size_t)(i + lane) * 4, lds + i * 4);
+  }
+}
+
+// Copy n floats global -> LDS with the whole workgroup by 4-byte LDS-DMA
+// (no alignment requirement beyond 4 bytes); caller waits vmcnt(0) + barrier.
+__device__ __forceinline__ void dma4_copy(const float* g, float* lds, int n, int wv, int lane) {
+  for (int i = wv * 64; i < n; i += kNT) {
+    if (i + lane < n)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + i + lane),
+                                       (__attribute__((address_space(3))) void*)(lds + i), 4, 0, 0);
   }
 }
 
@@ -193,6 +226,7 @@ __device__ __forceinline__ void attn_row_pass(float* A, int r, float* gout) {
 // Sum / max over the four 16-lane rows of a wave (lanes r, r+16, r+32, r+48),
 // identical bits in all four lanes: v_permlane32_swap + v_permlane16_swap.
 __device__ __forceinline__ float sum_rows4(float v) {
+  if (G2K_ABL & 1) return v;
   auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
   auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -209,61 +243,101 @@ __device__ __forceinline__ float max_rows4(float v) {
 // ---------------------------------------------------------------------------
 // Hidden recurrence (train.py:243-252), h in registers:
 //   h <- softmax(h, -1); h <- As @ h; adj <- softmax(h, -1) @ 1; h <- adj * h
-// computed as h'^T = softmax(h)^T @ As^T with v_mfma_f32_16x16x4_f32
-// (M = 16 columns of h, N = the 16 rows, K = 16 in four k-steps).  Wave w owns
-// columns [w*H/4, (w+1)*H/4) as TPW 16-wide tiles; lane l (r = l & 15,
-// q = l >> 4) holds ONE row r: h'[r][16t + 4q + i] in x[t][i].  Row softmax
-// sums are therefore a local sum plus a 2-step permlane reduction, and one
-// 4-wave LDS exchange per frame.  The next frame's A operand
-// (softmax(h)[k][c] with k on the lane group) is a wave-local 16x16
-// transpose through LDS (no barrier).
+// computed as h'^T = e^T @ (diag(1/Z) As^T) with v_mfma_f32_16x16x4_f32
+// (M = 16 columns of h, N = the 16 rows, K = 16 in four k-steps), where
+// e = exp(h) and Z its row sums (softmax = e / Z).  Wave w owns columns
+// [w*H/4, (w+1)*H/4) as TPW 16-wide tiles; lane l (r = l & 15, q = l >> 4)
+// holds ONE row r: h'[r][16t + 4q + i] in x[t][i].
 //
-// One exchange per frame: each wave publishes per-row P = sum e2 and
-// Q = sum h' * e2 (e2 = exp(h')).  Z2 = sum_w P_w, adj = sum_w P_w / Z2 (the
-// row sum of the softmax, evaluated from the wave partials), h_next =
-// adj * h', and the next softmax's numerators exp(adj * h') = e2 * exp(d h')
-// with d = adj - 1: |d| is a few ulp (adj == 1 in exact arithmetic) and h' is
-// in [0, 1] (convex combinations of softmax outputs), so exp(d h') =
-// 1 + d h' + O(1e-13) and the next row sums are P + d Q.
+// Per frame: (1) e goes through a wave-local 16x16 transpose in LDS into the
+// A-operand layout (no barrier); (2) the row sums Z_k of rows k = 4q..4q+3,
+// published by all four waves at the previous exchange, scale the B operand
+// As[r][k] / Z_k; (3) four MFMA k-steps per tile; (4) e2 = exp(h'), its per-row
+// partial sum (local + 2 permlane steps) is published for the next frame:
+// ONE 4-wave LDS exchange (one barrier) per frame.
+//
+// adj = sum_j softmax(h')_rj is evaluated from the published partials
+// (sum_w P_w / Z) and scales the final h.  The next frame's softmax needs
+// exp(adj * h'); |adj - 1| <= a few ulp (adj == 1 exactly in real arithmetic)
+// and h' lies in [0, 1] (convex combinations of softmax outputs), so in fp32
+// adj * h' is within one ulp of h' and exp(adj * h') is evaluated as
+// exp(h') = e2 (DESIGN.md "recurrence numerics"); the same bound makes the
+// tf.nn.softmax max shift the identity after frame 0.
 // ---------------------------------------------------------------------------
 constexpr int kTP = 20;            // transpose tile row pitch (floats): conflict-free b32 reads
 constexpr int kTTile = kD * kTP;   // 320 floats per 16x16 tile
 
-template <int TPW>
+template <int TPW, int NW>
 struct Recur {
-  float x[TPW][4];   // h (before init) / the last h' (after a step)
-  float e[TPW][4];   // numerators of the next softmax(h), row r
-  float rz;          // 1 / their row sum
-  float adj;         // row scale of the last step: h = adj * h'
+  static constexpr int kCols = 16 * TPW;   // columns per wave (H = NW * kCols)
+  float x[TPW][4];    // h (before init) / the last h' (after a step)
+  float e[TPW][4];    // numerators of the next softmax(h), row r
+  float av[TPW][4];   // e transposed into the A-operand layout: e[4q + ks][16t + r]
 
   __device__ __forceinline__ void load(const float* __restrict__ hs, int H, int wv, int q, int r) {
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-      const float4 v = *reinterpret_cast<const float4*>(hs + r * H + wv * (H / 4) + 16 * t + 4 * q);
+      const float4 v = *reinterpret_cast<const float4*>(hs + r * H + wv * kCols + 16 * t + 4 * q);
       x[t][0] = v.x; x[t][1] = v.y; x[t][2] = v.z; x[t][3] = v.w;
     }
-    adj = 1.0f;
   }
 
-  __device__ __forceinline__ void store(float* __restrict__ hs, int H, int wv, int q, int r) const {
+  // h = adj * h' with adj = row sum of softmax(h') from the last exchange
+  // (red: that frame's [4 waves][16 rows] partials), or h unchanged (nf == 0).
+  __device__ __forceinline__ void store(float* __restrict__ hs, int H, int wv, int q, int r,
+                                        const float* red) const {
+    float adj = 1.0f;
+    if (red) {
+      float z = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) z += red[16 * w + r];
+      const float rz = rcp(z);
+      adj = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) adj = fmaf(red[16 * w + r], rz, adj);
+    }
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
-      *reinterpret_cast<float4*>(hs + r * H + wv * (H / 4) + 16 * t + 4 * q) =
+      *reinterpret_cast<float4*>(hs + r * H + wv * kCols + 16 * t + 4 * q) =
           make_float4(adj * x[t][0], adj * x[t][1], adj * x[t][2], adj * x[t][3]);
   }
 
-  // softmax prologue on an arbitrary h (tf.nn.softmax max shift), 2 exchanges
-  // through `red` (128 floats used only here).
-  __device__ __forceinline__ void init(float* red, int wv, int q, int r) {
+  // e -> A-operand layout by a wave-local 16x16 transpose through LDS (sT:
+  // this wave's TPW tiles); LDS is in order within a wave, no barrier.
+  __device__ __forceinline__ void stage(float* sT, int q, int r) {
+    if (G2K_ABL & 16) {
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) av[t][ks] = e[t][ks];
+      return;
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+      *reinterpret_cast<float4*>(sT + t * kTTile + r * kTP + 4 * q) =
+          make_float4(e[t][0], e[t][1], e[t][2], e[t][3]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) av[t][ks] = sT[t * kTTile + (4 * q + ks) * kTP + r];
+  }
+
+  // softmax numerators of an arbitrary h (tf.nn.softmax max shift); publishes
+  // the row partial sums into `red` (64 floats) and stages e; barrier passed
+  // on return.  `mred`: 64 floats of scratch for the row max.
+  __device__ __forceinline__ void init(float* red, float* mred, float* sT, int wv, int q, int r) {
     float m = x[0][0];
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) m = fmaxf(m, x[t][i]);
     m = max_rows4(m);
-    if (q == 0) red[wv * 16 + r] = m;
+    if (q == 0) mred[wv * 16 + r] = m;
     __syncthreads();
-    m = fmaxf(fmaxf(red[r], red[16 + r]), fmaxf(red[32 + r], red[48 + r]));
+    m = mred[r];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) m = fmaxf(m, mred[16 * w + r]);
     float p = 0.f;
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
@@ -273,94 +347,119 @@ struct Recur {
         p += e[t][i];
       }
     p = sum_rows4(p);
-    if (q == 0) red[64 + wv * 16 + r] = p;
+    if (q == 0) red[wv * 16 + r] = p;
+    stage(sT, q, r);
     __syncthreads();
-    rz = rcp((red[64 + r] + red[80 + r]) + (red[96 + r] + red[112 + r]));
   }
 
-  // One frame.  b = As[r][4q..4q+3] of this frame (B operand: As^T[k][r]);
-  // as_next = next frame's As tile in LDS (or NULL), its slice is read after
-  // the barrier.  sT: this wave's TPW transpose tiles.  red: 128 floats,
-  // alternating between two buffers on consecutive frames.
-  __device__ __forceinline__ float4 step(const float4 b, const float* as_next, float* sT,
-                                         float* red, int wv, int q, int r) {
-    // A operand: softmax(h)[k = 4q + ks][c = 16t + r] via a wave-local transpose
+  // One frame.  b = As[r][4q..4q+3] of this frame; red_cur: the row partials
+  // of e (previous exchange); red_nxt: where this frame publishes its own.
+  __device__ __forceinline__ void step(const float4 b, const float* red_cur, float* red_nxt,
+                                       float* sT, int wv, int q, int r) {
+    RSTAMP(0);
+    // B operand: As[r][k] / Z_k, k = 4q + ks
+    float4 z = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (!(G2K_ABL & 4)) {
+      z = *reinterpret_cast<const float4*>(red_cur + 4 * q);
 #pragma unroll
-    for (int t = 0; t < TPW; ++t)
-      *reinterpret_cast<float4*>(sT + t * kTTile + r * kTP + 4 * q) =
-          make_float4(e[t][0] * rz, e[t][1] * rz, e[t][2] * rz, e[t][3] * rz);
-    __builtin_amdgcn_wave_barrier();
+      for (int w = 1; w < NW; ++w) {
+        const float4 v = *reinterpret_cast<const float4*>(red_cur + w * 16 + 4 * q);
+        z.x += v.x; z.y += v.y; z.z += v.z; z.w += v.w;
+      }
+    }
+    const float b0 = b.x * rcp(z.x);
+    const float b1 = b.y * rcp(z.y);
+    const float b2 = b.z * rcp(z.z);
+    const float b3 = b.w * rcp(z.w);
+    RSTAMP(1);
     f32x4 acc[TPW];
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      const float* col = sT + t * kTTile + (4 * q) * kTP + r;
-      f32x4 c = {0.f, 0.f, 0.f, 0.f};
-      c = __builtin_amdgcn_mfma_f32_16x16x4f32(col[0], b.x, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x4f32(col[kTP], b.y, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x4f32(col[2 * kTP], b.z, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x4f32(col[3 * kTP], b.w, c, 0, 0, 0);
-      acc[t] = c;
+    for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (G2K_ABL & 8) {
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+        acc[t] = f32x4{av[t][0] * b0, av[t][1] * b1, av[t][2] * b2, av[t][3] * b3};
+    } else {
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][0], b0, acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][1], b1, acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][2], b2, acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][3], b3, acc[t], 0, 0, 0);
     }
-    float p = 0.f, qs = 0.f;
+    RSTAMP(2);
+    float p = 0.f;
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float v = acc[t][i];
-        const float ex = __expf(v);       // h' in [0, 1]: no max shift needed
+        const float ex = (G2K_ABL & 32) ? v : __expf(v);   // h' in [0, 1]: no max shift needed
         x[t][i] = v;
         e[t][i] = ex;
         p += ex;
-        qs = fmaf(v, ex, qs);
       }
+    RSTAMP(3);
     p = sum_rows4(p);
-    qs = sum_rows4(qs);
-    if (q == 0) *reinterpret_cast<float2*>(red + wv * 32 + 2 * r) = make_float2(p, qs);
-    __syncthreads();
-    float4 nxt = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (as_next) nxt = *reinterpret_cast<const float4*>(as_next + r * kD + 4 * q);
-    const float2 w0 = *reinterpret_cast<const float2*>(red + 0 * 32 + 2 * r);
-    const float2 w1 = *reinterpret_cast<const float2*>(red + 1 * 32 + 2 * r);
-    const float2 w2 = *reinterpret_cast<const float2*>(red + 2 * 32 + 2 * r);
-    const float2 w3 = *reinterpret_cast<const float2*>(red + 3 * 32 + 2 * r);
-    const float r2 = rcp((w0.x + w1.x) + (w2.x + w3.x));
-    adj = (w0.x * r2 + w1.x * r2) + (w2.x * r2 + w3.x * r2);
-    const float d = adj - 1.0f;
-    rz = rcp((fmaf(d, w0.y, w0.x) + fmaf(d, w1.y, w1.x)) + (fmaf(d, w2.y, w2.x) + fmaf(d, w3.y, w3.x)));
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) e[t][i] = fmaf(e[t][i] * d, x[t][i], e[t][i]);
-    return nxt;
+    RSTAMP(4);
+    if (q == 0) red_nxt[wv * 16 + r] = p;
+    RSTAMP(5);
+    stage(sT, q, r);     // next frame's A operand, overlapping the barrier wait
+    RSTAMP(6);
+    if (!(G2K_ABL & 2)) __syncthreads();
+    RSTAMP(7);
+#ifdef G2K_STAMPS_RECUR
+    if (blockIdx.x == 0 && threadIdx.x == 0) g2k_rframe++;
+#endif
   }
 };
 
 // ---------------------------------------------------------------------------
-// Kernel 1: frame-parallel part.  LDS carve (floats; offsets multiple of 4).
+// Kernel 1: frame-parallel part.  One workgroup = 4 waves = kFramesPerWG
+// consecutive frames of one scene; one wave computes one frame.
+//
+// The workgroup stages the weights, lambda*G and the norms of its position
+// window in LDS and forms V = norms @ Wi for every window row (+ the two
+// vislet rows Ve) cooperatively; after that barrier every wave runs its frame
+// alone.  All the frame's small matmuls are v_mfma_f32_16x16x4_f32 chained in
+// registers: for D = A @ B the A operand of lane (L = lane & 15, q = lane >> 4)
+// at k-step ks is A[L][k], the B operand B[k][L], with k = 4q + ks, and the
+// result lands as D[4q + i][L] in register i — i.e. register ks of one result
+// is exactly the k-step-ks operand of a product that contracts over its row
+// index.  Each product below is oriented so that this holds:
+//   X0   = Wii @ U                       (U = V rows of the window)
+//   E    = Wv[:, :16] @ X0  (+ Ec + bv)  rows t on the lane group
+//   E^T  = X0^T @ Wv[:, :16]^T           rows t on the lane
+//   A    = g @ (E * Rm)                  -> As (train.py:240) -> workspace
+//   cost = E @ g
+//   M^T  = cost^T @ Wc^T   (x rows, y rows as two 16-wide tiles)
+//   Y^T  = Wo^T @ M^T      per 16 pedestrians -> pred_path_band, errors
+// (8-wide contractions use k-steps with zero rows: t = 4q + ks < 8.)
 // ---------------------------------------------------------------------------
+constexpr int kFramesPerWG = 4;
+
 struct FrameLayout {
   int np;   // padded norm row stride
-  int o_tgt, o_wi, o_wo, o_nrm, o_v, o_small, o_xa, o_e, o_c, o_m, o_met;
+  int o_wi, o_wo, o_nrm, o_v, o_small, o_y, o_pos, o_met;
   int total;
 };
 
 __host__ __device__ inline int rup4(int x) { return (x + 3) & ~3; }
 
-__host__ __device__ inline FrameLayout frame_layout(int Nmax, int stride, int fa) {
+__host__ __device__ inline FrameLayout frame_layout(int Nmax, int stride) {
   FrameLayout s;
-  const int wc = (fa - 1) * stride + kT;
+  const int wc = (kFramesPerWG - 1) * stride + kT;
   s.np = Nmax + 1;
   int o = 0;
-  s.o_tgt = o;   o += fa * Nmax * kL2;     // LDS-DMA destination
   s.o_wi = o;    o += rup4(Nmax * kD);
   s.o_wo = o;    o += rup4(kT * Nmax);
   s.o_nrm = o;   o += rup4((wc + 2) * s.np);
   s.o_v = o;     o += rup4((wc + 2) * kD);
   s.o_small = o; o += 1024;
-  s.o_xa = o;    o += fa * kD * kD;        // X0, then A / As
-  s.o_e = o;     o += fa * kT * kD;        // E
-  s.o_c = o;     o += fa * kT * kT;        // cost
-  s.o_m = o;     o += fa * kL2 * kT;       // Wc @ cost
+  s.o_y = o;     o += 4 * kD * kL2;         // per-wave prediction transpose [16 peds][12][2]
+  s.o_pos = o;   o += rup4(wc * Nmax * 2);  // raw position window (LDS-DMA)
   s.o_met = o;   o += 64;
   s.total = o;
   return s;
@@ -373,9 +472,7 @@ constexpr int SM_BV = 272;    // [16]
 constexpr int SM_WR = 288;    // [8][2]
 constexpr int SM_WC = 304;    // [24][8]  (192)
 constexpr int SM_G = 496;     // [16][8]  lambda * G
-constexpr int SM_RM = 624;    // [8][16]
-constexpr int SM_EC = 752;    // [8][16]  Wv[:,16:18] @ Ve
-// end 880 <= 1024
+// end 624 <= 1024
 
 struct StepArgs {
   g2k_dims d;
@@ -396,28 +493,37 @@ struct StepArgs {
   float* ws_as;        // [S, F, 16, 16] attention weights
   float* ws_part;      // [S, nchunk, 8] ADE/FDE partial sums
   float lambda;
-  int fchunk;
   int nchunk;
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// online (max, sum-of-exp) pair combine
+__device__ __forceinline__ void lse_combine(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
 __global__ void __launch_bounds__(kNT) g2k_frames_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int chunk = blockIdx.x, s = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, L = lane & 15, q = lane >> 4;
   const int Nmax = a.d.Nmax, W = a.d.W, F = a.d.F, stride = a.d.stride;
-  const int FA = a.fchunk;
   const int nact = clampi(a.n_active[s], 0, Nmax);
   const int nf = a.n_frames ? clampi(a.n_frames[s], 0, F) : F;
-  const int f0 = chunk * FA;
+  const int f0 = chunk * kFramesPerWG;
   float* part = a.ws_part + ((size_t)s * a.nchunk + chunk) * 8;
   STAMP(0);
 
   // frames of this chunk beyond n_frames: zero predictions
   {
     const int z0 = f0 > nf ? f0 : nf;
-    const int z1 = (f0 + FA) < F ? (f0 + FA) : F;
+    const int z1 = (f0 + kFramesPerWG) < F ? (f0 + kFramesPerWG) : F;
     for (int i = tid; i < (z1 - z0) * kL2 * Nmax; i += kNT)
       a.pred[((size_t)s * F + z0) * kL2 * Nmax + i] = 0.f;
   }
@@ -425,56 +531,53 @@ __global__ void __launch_bounds__(kNT) g2k_frames_kernel(StepArgs a) {
     if (tid < 8) part[tid] = 0.f;
     return;
   }
-  const int fa = (nf - f0) < FA ? (nf - f0) : FA;
+  const int fa = (nf - f0) < kFramesPerWG ? (nf - f0) : kFramesPerWG;
   const int r0 = f0 * stride, wc = (fa - 1) * stride + kT;
-  const FrameLayout lay = frame_layout(Nmax, stride, FA);
-  float* sTgt = smem + lay.o_tgt;
+  const FrameLayout lay = frame_layout(Nmax, stride);
+  // this wave's first-tile targets go in flight before the staging
+  float2 tgA[3] = {};
+  if (wv < fa) {
+    const int pp0 = lane >> 2, u0 = lane & 3;
+    const float2* tp = reinterpret_cast<const float2*>(
+        a.targets + (((size_t)s * F + f0 + wv) * Nmax + (pp0 < Nmax ? pp0 : 0)) * kL2) + 3 * u0;
+    tgA[0] = tp[0]; tgA[1] = tp[1]; tgA[2] = tp[2];
+  }
   float* sWi = smem + lay.o_wi;
   float* sWo = smem + lay.o_wo;
   float* sNrm = smem + lay.o_nrm;
   float* sV = smem + lay.o_v;
   float* sm = smem + lay.o_small;
-  float* sXA = smem + lay.o_xa;
-  float* sE = smem + lay.o_e;
-  float* sC = smem + lay.o_c;
-  float* sM = smem + lay.o_m;
   float* sMet = smem + lay.o_met;
+  float* sPos = smem + lay.o_pos;
   const int np = lay.np;
 
-  // ---- stage 0: targets by LDS-DMA; weights, vislet, window norms --------
-  dma_copy(a.targets + ((size_t)s * F + f0) * Nmax * kL2, sTgt, fa * Nmax * (kL2 / 4), wv, lane);
-  for (int i = tid; i < Nmax * kD; i += kNT) sWi[i] = (i / kD) < nact ? a.w.Wi[i] : 0.f;
-  for (int i = tid; i < kT * Nmax; i += kNT) sWo[i] = a.w.Wo[i];
-  if (tid < kD * kT) {
-    sm[SM_WII + tid] = a.w.Wii[tid];
-    sm[SM_G + tid] = a.lambda * a.G[(size_t)s * kD * kT + tid];   // ngh = lambda*ngh (g2k_lstm_mcr.py:102)
-  }
-  if (tid < kT * (kD + 2)) sm[SM_WV + tid] = a.w.Wv[tid];
-  if (tid < kD) sm[SM_BV + tid] = a.w.bv[tid];
-  if (tid < kT * 2) sm[SM_WR + tid] = a.w.Wr[tid];
-  if (tid < kL2 * kT) sm[SM_WC + tid] = a.w.Wc[tid];
+  // ---- staging by LDS-DMA (dword granules: any alignment), one wait -------
   {
+    dma4_copy(a.w.Wi, sWi, Nmax * kD, wv, lane);
+    dma4_copy(a.w.Wo, sWo, kT * Nmax, wv, lane);
+    dma4_copy(a.w.Wii, sm + SM_WII, kD * kT, wv, lane);
+    dma4_copy(a.G + (size_t)s * kD * kT, sm + SM_G, kD * kT, wv, lane);
+    dma4_copy(a.w.Wv, sm + SM_WV, kT * (kD + 2), wv, lane);
+    dma4_copy(a.w.bv, sm + SM_BV, kD, wv, lane);
+    dma4_copy(a.w.Wr, sm + SM_WR, kT * 2, wv, lane);
+    dma4_copy(a.w.Wc, sm + SM_WC, kL2 * kT, wv, lane);
     const float* vis = a.vislet + (size_t)s * 2 * Nmax;
-    for (int i = tid; i < 2 * Nmax; i += kNT) {
-      const int c = i / Nmax, n = i - c * Nmax;
-      sNrm[(wc + c) * np + n] = n < nact ? vis[i] : 0.f;
-    }
-    const float2* p2 = reinterpret_cast<const float2*>(a.pos) + ((size_t)s * W + r0) * Nmax;
-    for (int i = tid; i < wc * Nmax; i += kNT) {
-      const int w = i / Nmax, n = i - w * Nmax;
-      float v = 0.f;
-      if (n < nact) {
-        const float2 p = p2[i];
-        v = sqrtf(fmaf(p.x, p.x, p.y * p.y));     // ||(x, y)||_2 (train.py:79)
-      }
-      sNrm[w * np + n] = v;
-    }
+    dma4_copy(vis, sNrm + wc * np, Nmax, wv, lane);
+    dma4_copy(vis + Nmax, sNrm + (wc + 1) * np, Nmax, wv, lane);
+    dma4_copy(a.pos + ((size_t)s * W + r0) * Nmax * 2, sPos, wc * Nmax * 2, wv, lane);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // window norms ||(x, y)||_2 (train.py:79); ngh = lambda * ngh (g2k_lstm_mcr.py:102)
+  for (int i = tid; i < wc * Nmax; i += kNT) {
+    const int w = i / Nmax, n = i - w * Nmax;
+    const float2 p = reinterpret_cast<const float2*>(sPos)[i];
+    sNrm[w * np + n] = n < nact ? sqrtf(fmaf(p.x, p.x, p.y * p.y)) : 0.f;
+  }
+  if (tid < kD * kT) sm[SM_G + tid] *= a.lambda;
   __syncthreads();
   STAMP(1);
-
-  // ---- stage 1: V = nrm @ Wi for the chunk's position rows (+ Ve rows) ----
-  // frame f's Bv @ Wi (train.py:179) is rows (f-f0)*stride .. +7 of V.
+  // ---- V = norms @ Wi (train.py:179 for every window row) and Ve rows -----
   {
     const int dcol = tid & 15;
     for (int w = tid >> 4; w < wc + 2; w += kNT / 16) {
@@ -492,122 +595,196 @@ __global__ void __launch_bounds__(kNT) g2k_frames_kernel(StepArgs a) {
     }
   }
   __syncthreads();
-  // ---- stage 2: per-scene Rel/Rm and the Ve part of E ---------------------
-  if (tid < kT * kD) {
-    const int t = tid >> 4, dcol = tid & 15;
-    const float ve0 = sV[wc * kD + dcol], ve1 = sV[(wc + 1) * kD + dcol];
-    // Rel = Ve * Ve (train.py:194-195); Rm = Wr @ Rel (g2k_lstm_mcr.py:106)
-    sm[SM_RM + tid] = fmaf(sm[SM_WR + 2 * t], ve0 * ve0, sm[SM_WR + 2 * t + 1] * (ve1 * ve1));
-    sm[SM_EC + tid] = fmaf(sm[SM_WV + t * (kD + 2) + kD], ve0, sm[SM_WV + t * (kD + 2) + kD + 1] * ve1);
-  }
-  // ---- stage 3: X0_f = Wii @ U_f  (train.py:180) -------------------------
-  {
-    const int dcol = tid & 15, k = tid >> 4;
-    float wii[kT];
-#pragma unroll
-    for (int t = 0; t < kT; ++t) wii[t] = sm[SM_WII + k * kT + t];
-    for (int fl = 0; fl < fa; ++fl) {
-      const float* v = sV + (fl * stride) * kD + dcol;
-      float x = 0.f;
-#pragma unroll
-      for (int t = 0; t < kT; ++t) x = fmaf(wii[t], v[t * kD], x);
-      sXA[fl * kD * kD + k * kD + dcol] = x;
-    }
-  }
-  __syncthreads();
   STAMP(2);
-  // ---- stage 4: E_f = Wv @ [X0_f; Ve] + bv  (g2k_lstm_mcr.py:105,112) ------
-  {
-    const int dcol = tid & 15, t = (tid >> 4) & 7;
-    float wv16[kD];
-#pragma unroll
-    for (int k = 0; k < kD; ++k) wv16[k] = sm[SM_WV + t * (kD + 2) + k];
-    const float ec = sm[SM_EC + t * kD + dcol];
-    const float bvv = sm[SM_BV + dcol];
-    for (int fl = tid >> 7; fl < fa; fl += 2) {
-      const float* x0 = sXA + fl * kD * kD + dcol;
-      float e = 0.f;
-#pragma unroll
-      for (int k = 0; k < kD; ++k) e = fmaf(wv16[k], x0[k * kD], e);
-      sE[fl * kT * kD + t * kD + dcol] = (e + ec) + bvv;
-    }
-  }
-  __syncthreads();
-  STAMP(3);
-  // ---- stage 5: A_f = g @ (E_f * Rm), cost_f = E_f @ g  (:105-106, :112) ---
-  {
-    const int dcol = tid & 15, r = tid >> 4;
-    float gr[kT], rm[kT];
-#pragma unroll
-    for (int t = 0; t < kT; ++t) { gr[t] = sm[SM_G + r * kT + t]; rm[t] = sm[SM_RM + t * kD + dcol]; }
-    for (int fl = 0; fl < fa; ++fl) {
-      const float* e = sE + fl * kT * kD + dcol;
-      float x = 0.f;
-#pragma unroll
-      for (int t = 0; t < kT; ++t) x = fmaf(gr[t], e[t * kD] * rm[t], x);
-      sXA[fl * kD * kD + r * kD + dcol] = x;
-      if (a.A_out) a.A_out[(((size_t)s * F + f0 + fl) * kD + r) * kD + dcol] = x;
-    }
-    const int t2 = tid & 7, t1 = (tid >> 3) & 7;
-    float gc[kD];
-#pragma unroll
-    for (int k = 0; k < kD; ++k) gc[k] = sm[SM_G + k * kT + t2];
-    for (int fl = tid >> 6; fl < fa; fl += 4) {
-      const float* e = sE + fl * kT * kD + t1 * kD;
-      float x = 0.f;
-#pragma unroll
-      for (int k = 0; k < kD; ++k) x = fmaf(e[k], gc[k], x);
-      sC[fl * kT * kT + t1 * kT + t2] = x;
-      if (a.cost_out) a.cost_out[(((size_t)s * F + f0 + fl) * kT + t1) * kT + t2] = x;
-    }
-  }
-  __syncthreads();
-  STAMP(4);
-  // ---- stage 6: attention column pass; M_f = Wc @ cost_f (:122) ------------
-  for (int task = tid; task < fa * kD; task += kNT)
-    attn_column_pass(sXA + (task >> 4) * kD * kD, task & 15);
-  for (int task = tid; task < fa * kL2 * kT; task += kNT) {
-    const int fl = task / (kL2 * kT), rem = task - fl * kL2 * kT;
-    const int jr = rem >> 3, t2 = rem & 7;
-    const float* c = sC + fl * kT * kT + t2;
-    float x = 0.f;
-#pragma unroll
-    for (int t = 0; t < kT; ++t) x = fmaf(sm[SM_WC + jr * kT + t], c[t * kT], x);
-    sM[fl * kL2 * kT + rem] = x;
-  }
-  // the DMA'd targets are read in stage 7
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  STAMP(5);
-  // ---- stage 7: attention row softmax -> workspace; pred = M_f @ Wo; errors -
-  for (int task = tid; task < fa * kD; task += kNT) {
-    const int fl = task >> 4;
-    attn_row_pass(sXA + fl * kD * kD, task & 15,
-                  a.ws_as + ((size_t)s * F + f0 + fl) * kD * kD);
-  }
+
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int task = tid; task < fa * Nmax; task += kNT) {
-    const int fl = task / Nmax, n = task - fl * Nmax;
-    float* pp = a.pred + ((size_t)s * F + f0 + fl) * kL2 * Nmax + n;
-    if (n < nact) {
-      float wo[kT];
+  if (wv < fa) {
+    const int f = f0 + wv;
+    const float* vw = sV + (wv * stride) * kD;       // U = rows of this frame's window
+    const float ve0 = sV[wc * kD + L], ve1 = sV[(wc + 1) * kD + L];   // Ve[:, d = L]
+    const bool kq = q < 2;                           // k = 4q + ks < 8
+
+    // X0 = Wii @ U   (train.py:180): k = 4ks + q over the 8 window rows
+    f32x4 x0 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < kT; ++t) wo[t] = sWo[t * Nmax + n];
-      float y[kL2];
-      const float* m = sM + fl * kL2 * kT;
+    for (int ks = 0; ks < 2; ++ks)
+      x0 = mfma4(sm[SM_WII + L * kT + 4 * ks + q], vw[(4 * ks + q) * kD + L], x0);
+    // E = Wv[:, :16] @ X0 (+ Wv[:, 16:18] @ Ve + bv)  (g2k_lstm_mcr.py:105,112)
+    float wv16[4];
 #pragma unroll
-      for (int jr = 0; jr < kL2; ++jr) {
-        float x = 0.f;
+    for (int ks = 0; ks < 4; ++ks) wv16[ks] = L < kT ? sm[SM_WV + L * (kD + 2) + 4 * q + ks] : 0.f;
+    f32x4 eN = {0.f, 0.f, 0.f, 0.f}, eT = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < kT; ++t) x = fmaf(m[jr * kT + t], wo[t], x);
-        y[jr] = x;
-        pp[jr * Nmax] = x;        // pred_path_band = reshape(temp, (2, 12, N))
+    for (int ks = 0; ks < 4; ++ks) {
+      eN = mfma4(wv16[ks], x0[ks], eN);      // E[4q+i][L]
+      eT = mfma4(x0[ks], wv16[ks], eT);      // E[L][4q+i]
+    }
+    const float bvL = sm[SM_BV + L];
+    // Rel = Ve * Ve (train.py:194-195), Rm = Wr @ Rel (g2k_lstm_mcr.py:106)
+    float em[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 4 * q + i;
+      if (kq) {
+        eN[i] = (eN[i] + fmaf(sm[SM_WV + t * (kD + 2) + kD], ve0,
+                              sm[SM_WV + t * (kD + 2) + kD + 1] * ve1)) + bvL;
+        const float rm = fmaf(sm[SM_WR + 2 * t], ve0 * ve0, sm[SM_WR + 2 * t + 1] * (ve1 * ve1));
+        em[i] = eN[i] * rm;
+      } else {
+        em[i] = 0.f;
       }
-      const bool has_t = a.ped_mask ? (a.ped_mask[(size_t)s * Nmax + n] != 0) : true;
-      if (has_t) error_terms(y, sTgt + (fl * Nmax + n) * kL2, acc);
-    } else {
+    }
+    if (L < kT) {
+      const float w16 = sm[SM_WV + L * (kD + 2) + kD], w17 = sm[SM_WV + L * (kD + 2) + kD + 1];
 #pragma unroll
-      for (int jr = 0; jr < kL2; ++jr) pp[jr * Nmax] = 0.f;
+      for (int i = 0; i < 4; ++i) {
+        const int d = 4 * q + i;
+        eT[i] = (eT[i] + fmaf(w16, sV[wc * kD + d], w17 * sV[(wc + 1) * kD + d])) +
+                sm[SM_BV + d];
+      }
+    }
+    // A = g @ (E * Rm)  (g2k_lstm_mcr.py:105-106); cost = E @ g (:112-113)
+    f32x4 aA = {0.f, 0.f, 0.f, 0.f}, cC = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const float gA = kq ? sm[SM_G + L * kT + 4 * q + ks] : 0.f;            // g[r = L][t]
+      const float gB = L < kT ? sm[SM_G + (4 * q + ks) * kT + L] : 0.f;      // g[d][t2 = L]
+      aA = mfma4(gA, em[ks], aA);      // A[4q+i][L]
+      cC = mfma4(eT[ks], gB, cC);      // cost[4q+i][L]
+    }
+    if (a.A_out) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a.A_out[(((size_t)s * F + f) * kD + 4 * q + i) * kD + L] = aA[i];
+    }
+    if (a.cost_out && kq && L < kT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a.cost_out[(((size_t)s * F + f) * kT + 4 * q + i) * kT + L] = cC[i];
+    }
+    // As = softmax(exp(A) / cumsum(exp(A), axis 0), axis -1)  (train.py:240)
+    // column L, rows 4q+i: running (max, sum exp) down the rows, exclusive
+    // prefix over the four lane groups, then a 16-lane row softmax.
+    {
+      float m_i[4], s_i[4];
+      float m = -INFINITY, sacc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lse_combine(m, sacc, aA[i], 1.0f);
+        m_i[i] = m; s_i[i] = sacc;
+      }
+      float mp = -INFINITY, sp = 0.f;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const float mg = __shfl(m, L + 16 * g, 64);
+        const float sg = __shfl(sacc, L + 16 * g, 64);
+        if (g < q) lse_combine(mp, sp, mg, sg);
+      }
+      float ex[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float mr = m_i[i], sr = s_i[i];
+        if (q > 0) lse_combine(mr, sr, mp, sp);
+        const float R = __expf(aA[i] - mr) * rcp(sr);     // in (0, 1]
+        ex[i] = __expf(R);
+      }
+      float* as = a.ws_as + ((size_t)s * F + f) * kD * kD;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) as[(4 * q + i) * kD + L] = ex[i] * rcp(row16_sum(ex[i]));
+    }
+    // M^T = cost^T @ Wc^T for the x rows (jt 0) and y rows (jt 1) of temp_path
+    f32x4 mT0 = {0.f, 0.f, 0.f, 0.f}, mT1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bool ok = kq && L < kL;
+      const float wc0 = ok ? sm[SM_WC + L * kT + 4 * q + ks] : 0.f;
+      const float wc1 = ok ? sm[SM_WC + (kL + L) * kT + 4 * q + ks] : 0.f;
+      mT0 = mfma4(cC[ks], wc0, mT0);   // M[L][4q+i]       (x rows)
+      mT1 = mfma4(cC[ks], wc1, mT1);   // M[12+L][4q+i]    (y rows)
+    }
+    // Y^T = Wo^T @ M^T per 16 pedestrians; pred_path_band = reshape(Y, (2,12,N))
+    float* ys = smem + lay.o_y + wv * kD * kL2;
+    const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
+    const int pp = lane >> 2, u = lane & 3;             // error lanes: pedestrian, quarter
+    const float* tgt_f = a.targets + ((size_t)s * F + f) * Nmax * kL2;
+    float* pr = a.pred + ((size_t)s * F + f) * kL2 * Nmax;
+    const int ntiles = (Nmax + 15) / 16;
+    // targets of tiles t and t+1 are in flight while tile t is computed
+    float2 tgB[3];
+    auto load_tg = [&](int t, float2 (&tg)[3]) {
+      const int ne = 16 * t + pp;
+      const int nc = ne < Nmax ? ne : 0;
+      const float2* tp = reinterpret_cast<const float2*>(tgt_f + (size_t)nc * kL2) + 3 * u;
+      tg[0] = tp[0]; tg[1] = tp[1]; tg[2] = tp[2];
+    };
+    auto tile = [&](int t, const float2 (&tg)[3]) {
+      const int n0 = 16 * t;
+      const int ne = n0 + pp;
+      const bool has_t = ne < nact && (pm ? pm[ne] != 0 : true);
+      f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int n = n0 + L;
+        const float wo = (kq && n < nact) ? sWo[(4 * q + ks) * Nmax + n] : 0.f;
+        y0 = mfma4(wo, mT0[ks], y0);   // Y[L][n0 + 4q + i]
+        y1 = mfma4(wo, mT1[ks], y1);   // Y[12 + L][n0 + 4q + i]
+      }
+      if (L < kL) {
+        const int nb = n0 + 4 * q;
+        if (nb + 3 < Nmax && ((Nmax & 3) == 0)) {
+          *reinterpret_cast<float4*>(pr + L * Nmax + nb) = make_float4(y0[0], y0[1], y0[2], y0[3]);
+          *reinterpret_cast<float4*>(pr + (kL + L) * Nmax + nb) = make_float4(y1[0], y1[1], y1[2], y1[3]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (nb + i < Nmax) { pr[L * Nmax + nb + i] = y0[i]; pr[(kL + L) * Nmax + nb + i] = y1[i]; }
+        }
+        // transpose to [16 peds][12 steps][2] for the error lanes
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<float2*>(ys + (4 * q + i) * kL2 + 2 * L) = make_float2(y0[i], y1[i]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      // a9 errors (train.py:640-656): 4 lanes per pedestrian, 3 steps each
+      float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f, fx = 0.f, fy = 0.f;
+      const float2* yp = reinterpret_cast<const float2*>(ys + pp * kL2) + 3 * u;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float2 yv = yp[k];
+        const float dx = yv.x - tg[k].x, dy = yv.y - tg[k].y;
+        ea = fmaf(dx, dx, ea);
+        eb = fmaf(dx, dy, eb);
+        ec = fmaf(dy, dy, ec);
+        el2 += sqrtf(fmaf(dx, dx, dy * dy));
+        fx = dx; fy = dy;
+      }
+      __builtin_amdgcn_wave_barrier();
+      // quad sums; the fde vector (step 11) lives in quarter 3
+      ea += dpp<0xB1>(ea); ea += dpp<0x4E>(ea);
+      eb += dpp<0xB1>(eb); eb += dpp<0x4E>(eb);
+      ec += dpp<0xB1>(ec); ec += dpp<0x4E>(ec);
+      el2 += dpp<0xB1>(el2); el2 += dpp<0x4E>(el2);
+      fx = dpp<0xFF>(fx);   // quad_perm [3,3,3,3]
+      fy = dpp<0xFF>(fy);
+      if (has_t && u == 0) {
+        const float hm = 0.5f * (ea - ec);
+        const float lam = 0.5f * (ea + ec) + sqrtf(fmaf(hm, hm, eb * eb));
+        const float fsq = fmaf(fx, fx, fy * fy);
+        acc[0] += sqrtf(fmaxf(lam, 0.f)) * (1.0f / 12.0f);
+        acc[1] += 1.0f;
+        acc[2] += fsq;
+        acc[3] += el2 * (1.0f / 12.0f);
+        acc[4] += sqrtf(fsq);
+      }
+    };
+    load_tg(1 < ntiles ? 1 : 0, tgB);
+    for (int t = 0; t < ntiles; t += 2) {
+      tile(t, tgA);
+      if (t + 2 < ntiles) load_tg(t + 2, tgA);
+      if (t + 1 < ntiles) {
+        tile(t + 1, tgB);
+        if (t + 3 < ntiles) load_tg(t + 3, tgB);
+      }
     }
   }
   // ---- ADE/FDE partial sums of this chunk: fixed order, no atomics --------
@@ -636,16 +813,23 @@ struct RecurArgs {
   int F, H, nchunk, raw_attn;
 };
 
-template <int TPW>
-__global__ void __launch_bounds__(kNT) g2k_recur_kernel(RecurArgs a) {
+template <int TPW, int NW>
+__global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(RecurArgs a) {
+  constexpr int kRT = 64 * NW;               // threads
+  constexpr int kRB = 16 * NW;               // floats per row-partial buffer
   __shared__ __attribute__((aligned(16))) float sAs[kRecurChunk * kD * kD];
-  __shared__ __attribute__((aligned(16))) float sRed[2 * 128 + 128];
-  __shared__ __attribute__((aligned(16))) float sT[4 * TPW * kTTile];
+  __shared__ __attribute__((aligned(16))) float sRed[4 * kRB];
+  __shared__ __attribute__((aligned(16))) float sT[NW * TPW * kTTile];
   const int s = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6, q = lane >> 4, j = lane & 15;
   const int F = a.F, H = a.H;
   const int nf = a.n_frames ? clampi(a.n_frames[s], 0, F) : F;
   STAMP(10);
+  // first As chunk, h and the metric partials all in flight together
+  const int cnt0 = nf < kRecurChunk ? nf : kRecurChunk;
+  if (nf > 0) dma_copy_n<kRT>(a.att + (size_t)s * F * kD * kD, sAs, cnt0 * (kD * kD / 4), wv, lane);
+  Recur<TPW, NW> rec;
+  rec.load(a.h_in + (size_t)s * kD * H, H, wv, q, j);
   if (a.metrics && tid < 8) {
     float v = 0.f;
     if (tid < 5) {
@@ -656,33 +840,38 @@ __global__ void __launch_bounds__(kNT) g2k_recur_kernel(RecurArgs a) {
     }
     a.metrics[(size_t)s * 8 + tid] = v;
   }
-  Recur<TPW> rec;
-  rec.load(a.h_in + (size_t)s * kD * H, H, wv, q, j);
+  float* sTw = sT + wv * TPW * kTTile;
+  // sRed: three row-partial buffers rotated per frame + one for the row max
+  const float* last = nullptr;
   if (nf > 0) {
-    rec.init(sRed + 256, wv, q, j);
+    rec.init(sRed, sRed + 3 * kRB, sTw, wv, q, j);
+    int cur = 0;
     for (int fb = 0; fb < nf; fb += kRecurChunk) {
       const int cnt = (nf - fb) < kRecurChunk ? (nf - fb) : kRecurChunk;
-      dma_copy(a.att + ((size_t)s * F + fb) * kD * kD, sAs, cnt * (kD * kD / 4), wv, lane);
+      if (fb > 0) dma_copy_n<kRT>(a.att + ((size_t)s * F + fb) * kD * kD, sAs, cnt * (kD * kD / 4), wv, lane);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (a.raw_attn) {
-        for (int task = tid; task < cnt * kD; task += kNT)
+        for (int task = tid; task < cnt * kD; task += kRT)
           attn_column_pass(sAs + (task >> 4) * kD * kD, task & 15);
         __syncthreads();
-        for (int task = tid; task < cnt * kD; task += kNT)
+        for (int task = tid; task < cnt * kD; task += kRT)
           attn_row_pass(sAs + (task >> 4) * kD * kD, task & 15, nullptr);
         __syncthreads();
       }
       STAMP(11);
-      float4 arow = *reinterpret_cast<const float4*>(sAs + j * kD + 4 * q);
-      for (int fl = 0; fl < cnt; ++fl)
-        arow = rec.step(arow, fl + 1 < cnt ? sAs + (fl + 1) * kD * kD : nullptr,
-                        sT + wv * TPW * kTTile, sRed + ((fb + fl) & 1) * 128, wv, q, j);
+      for (int fl = 0; fl < cnt; ++fl) {
+        const float4 b = *reinterpret_cast<const float4*>(sAs + fl * kD * kD + j * kD + 4 * q);
+        const int nxt = cur == 2 ? 0 : cur + 1;
+        rec.step(b, sRed + cur * kRB, sRed + nxt * kRB, sTw, wv, q, j);
+        cur = nxt;
+      }
+      last = sRed + cur * kRB;
       __syncthreads();   // all waves done with sAs before the next DMA
     }
   }
   STAMP(12);
-  rec.store(a.h_out + (size_t)s * kD * H, H, wv, q, j);
+  rec.store(a.h_out + (size_t)s * kD * H, H, wv, q, j, last);
 }
 
 // ---------------------------------------------------------------------------
@@ -892,39 +1081,48 @@ int validate_weights(const g2k_weights* w, bool need_embed) {
   return G2K_OK;
 }
 
-// Frames per g2k_frames_kernel workgroup: the largest chunk (<= 8) whose LDS
-// carve stays within kFramesLdsBudget (>= 3 workgroups per CU), then
-// balanced over the chunks.
 struct StepPlan {
-  int fchunk, nchunk;
+  int nchunk;
   int64_t lds_bytes, ws_bytes;
 };
 
 StepPlan plan_step(const g2k_dims* d) {
-  StepPlan p = {0, 0, 0, 0};
+  StepPlan p = {0, 0, 0};
   const int F = d->F < 1 ? 1 : d->F;
-  int best = 1;
-  for (int fa = (F < 8 ? F : 8); fa >= 1; --fa) {
-    if ((int64_t)frame_layout(d->Nmax, d->stride, fa).total * 4 <= kFramesLdsBudget) {
-      best = fa;
-      break;
-    }
-  }
-  p.nchunk = (F + best - 1) / best;
-  p.fchunk = (F + p.nchunk - 1) / p.nchunk;
-  p.lds_bytes = (int64_t)frame_layout(d->Nmax, d->stride, p.fchunk).total * 4;
+  p.nchunk = (F + kFramesPerWG - 1) / kFramesPerWG;
+  p.lds_bytes = (int64_t)frame_layout(d->Nmax, d->stride).total * 4;
   const int64_t as_bytes = (int64_t)d->S * (d->F > 0 ? d->F : 0) * kD * kD * 4;
   p.ws_bytes = as_bytes + (int64_t)d->S * p.nchunk * 8 * 4;
   return p;
 }
 
+// Waves per recurrence workgroup: 8 (two per SIMD, so one wave's latency
+// hides under the other's issue) whenever H allows 16-column tiles per wave.
+int recur_waves(int H) {
+  const char* env = getenv("G2K_RECUR_WAVES");   // tuning override (4 or 8)
+  if (env && (atoi(env) == 4 || (atoi(env) == 8 && H >= 128))) return atoi(env);
+  return H >= 128 ? 8 : 4;
+}
+
 int launch_recur(const RecurArgs& r, int S, hipStream_t st) {
-  switch (r.H / 64) {
-    case 1: hipLaunchKernelGGL(g2k_recur_kernel<1>, dim3(S), dim3(kNT), 0, st, r); break;
-    case 2: hipLaunchKernelGGL(g2k_recur_kernel<2>, dim3(S), dim3(kNT), 0, st, r); break;
-    case 4: hipLaunchKernelGGL(g2k_recur_kernel<4>, dim3(S), dim3(kNT), 0, st, r); break;
-    case 8: hipLaunchKernelGGL(g2k_recur_kernel<8>, dim3(S), dim3(kNT), 0, st, r); break;
-    default: return set_err(G2K_EUNSUPPORTED, "H=%d: H/64 must be 1, 2, 4 or 8", r.H);
+  const int nw = recur_waves(r.H);
+  const int tpw = r.H / (16 * nw);
+  dim3 g(S);
+  if (nw == 4) {
+    switch (tpw) {
+      case 1: hipLaunchKernelGGL((g2k_recur_kernel<1, 4>), g, dim3(256), 0, st, r); break;
+      case 2: hipLaunchKernelGGL((g2k_recur_kernel<2, 4>), g, dim3(256), 0, st, r); break;
+      case 4: hipLaunchKernelGGL((g2k_recur_kernel<4, 4>), g, dim3(256), 0, st, r); break;
+      case 8: hipLaunchKernelGGL((g2k_recur_kernel<8, 4>), g, dim3(256), 0, st, r); break;
+      default: return set_err(G2K_EUNSUPPORTED, "H=%d unsupported", r.H);
+    }
+  } else {
+    switch (tpw) {
+      case 1: hipLaunchKernelGGL((g2k_recur_kernel<1, 8>), g, dim3(512), 0, st, r); break;
+      case 2: hipLaunchKernelGGL((g2k_recur_kernel<2, 8>), g, dim3(512), 0, st, r); break;
+      case 4: hipLaunchKernelGGL((g2k_recur_kernel<4, 8>), g, dim3(512), 0, st, r); break;
+      default: return set_err(G2K_EUNSUPPORTED, "H=%d unsupported", r.H);
+    }
   }
   return G2K_OK;
 }
@@ -949,6 +1147,16 @@ int g2k_abi_version(void) { return G2K_ABI_VERSION; }
 
 const char* g2k_last_error(void) { return g_err; }
 
+#ifdef G2K_STAMPS_RECUR
+int g2k_debug_rstamps(unsigned long long* host) {
+  int z = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(g2k_rframe), &z, sizeof(int));
+  return 0;
+}
+int g2k_debug_rstamps_get(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2k_rstamps), 16 * sizeof(unsigned long long));
+}
+#endif
 #ifdef G2K_STAMPS
 int g2k_debug_stamps(unsigned long long* host, int n) {
   if (n > 64) n = 64;
@@ -986,6 +1194,9 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
   if (((uintptr_t)pos & 7u) != 0) return set_err(G2K_EINVAL, "pos must be 8-byte aligned");
   if (d->S == 0) return G2K_OK;
   const StepPlan p = plan_step(d);
+  if (p.lds_bytes > 160 * 1024)
+    return set_err(G2K_ELDS, "Nmax=%d, stride=%d needs %lld bytes of LDS", d->Nmax, d->stride,
+                   (long long)p.lds_bytes);
   if (!workspace || workspace_bytes < p.ws_bytes)
     return set_err(G2K_EINVAL, "workspace of %lld bytes needed (got %lld)", (long long)p.ws_bytes,
                    (long long)workspace_bytes);
@@ -993,7 +1204,7 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
   a.d = *d; a.w = *w; a.pos = pos; a.vislet = vislet; a.G = G; a.targets = targets;
   a.n_active = n_active; a.n_frames = n_frames; a.ped_mask = ped_mask; a.h_in = h_in;
   a.h_out = h_out; a.pred = pred; a.metrics = metrics; a.A_out = A_out; a.cost_out = cost_out;
-  a.lambda = lambda; a.fchunk = p.fchunk; a.nchunk = p.nchunk;
+  a.lambda = lambda; a.nchunk = p.nchunk;
   a.ws_as = static_cast<float*>(workspace);
   a.ws_part = a.ws_as + (size_t)d->S * d->F * kD * kD;
   hipStream_t st = (hipStream_t)stream;

@@ -12,8 +12,7 @@ subprocess.run([build.HIPCC, *build.FLAGS, "-DG2K_STAMPS", "-o", out, *build.SRC
 lib = _lib.load(out)
 _lib._lib = lib
 lib.g2k_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-names = {1: "A stage0 load+DMA issue", 2: "A stage1-3 V,Rm,X0", 3: "A stage4 E", 4: "A stage5 A,cost",
-         5: "A stage6 col,M + DMA wait", 6: "A stage7 row,pred,err,reduce",
+names = {1: "A staging (weights, norms)", 2: "A V = norms @ Wi", 6: "A per-wave frames + reduce",
          11: "B metrics,h load,init,As DMA", 12: "B recurrence frames"}
 for cfg in sys.argv[1:] or ["eth_hotel_synth"]:
     c = CONFIGS[cfg]
@@ -30,5 +29,5 @@ for cfg in sys.argv[1:] or ["eth_hotel_synth"]:
     v = np.array(st[:13], dtype=np.int64)
     print(f"== {cfg} (S={S}) n_active[0]={b.n_active[0]}  frames-kernel WG(0,0) {v[6]-v[0]} ticks, "
           f"recur WG 0 {v[12]-v[10]} ticks")
-    for k in (1, 2, 3, 4, 5, 6, 11, 12):
-        print(f"  {names[k]:32s} {v[k]-v[k-1]:8d}")
+    for k, k0 in ((1, 0), (2, 1), (6, 2), (11, 10), (12, 11)):
+        print(f"  {names[k]:32s} {v[k]-v[k0]:8d}")
