@@ -1,0 +1,42 @@
+"""Data parallelism over scene batches.
+
+Scenes are independent (no cross-scene term in a1-a9), so every rank owns a
+contiguous shard of scenes and runs the HIP step on it with no data-path
+collective ("replicas only").  The only exchange is the sum of the ADE/FDE
+numerators and counts, once per reporting interval — one tiny all-reduce
+(RCCL on ROCm when the backend is "nccl", gloo on CPU).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_scenes(total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous [start, stop) of ``total`` scenes for ``rank`` (sizes differ
+    by at most one)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"rank {rank} / world {world}")
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def reduce_metrics(metrics: torch.Tensor, group=None) -> torch.Tensor:
+    """Per-scene metric rows [S, 8] -> the all-rank sum [8] (float64).
+    Field order: see frame_step.METRIC_FIELDS."""
+    tot = metrics.to(torch.float64).sum(dim=0)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
+    return tot
+
+
+def global_errors(tot: torch.Tensor):
+    """(ADE, FDE) over everything summed by reduce_metrics: ADE = mean of the
+    per-(frame, pedestrian) spectral ade_i (train.py:648-669); FDE = Frobenius
+    norm of the stacked fde vectors over the number of frames (train.py:674)."""
+    t = tot.double().cpu()
+    cnt = float(t[1])
+    if cnt <= 0:
+        return float("nan"), float("nan")
+    return float(t[0] / cnt), float(torch.sqrt(t[2]) / max(float(t[5]), 1.0))

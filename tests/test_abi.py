@@ -1,0 +1,82 @@
+"""The C-ABI library loads, exports every symbol include/g2k_hip.h declares,
+and rejects bad arguments before touching the GPU (runs on CPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from multimodaltraj_2_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "g2k_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(g2k_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    assert sorted(_lib.SYMBOLS) == declared_functions()
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.g2k_abi_version() == _lib.ABI_VERSION
+
+
+def _dims(**kw):
+    d = dict(S=2, F=20, T=8, L=12, D=16, H=128, Nmax=32, W=27, stride=1)
+    d.update(kw)
+    return _lib.G2KDims(**d)
+
+
+@pytest.mark.parametrize("bad,code", [(dict(T=10), -4), (dict(D=10), -4), (dict(H=96), -4),
+                                      (dict(Nmax=0), -1), (dict(Nmax=300), -1), (dict(W=26), -1),
+                                      (dict(stride=-1), -1), (dict(S=-1), -1)])
+def test_step_rejects_bad_geometry(bad, code):
+    lib = _lib.load()
+    w = _lib.G2KWeights(*([ctypes.c_void_p(16)] * 7))
+    p = ctypes.c_void_p(16)
+    rc = lib.g2k_step_fused_f32(ctypes.byref(_dims(**bad)), ctypes.byref(w), p, p, p, p, p, None,
+                                None, p, p, p, p, None, None, 5e-4, p, 1 << 30, None)
+    assert rc == code
+    assert lib.g2k_last_error()
+
+
+def test_step_rejects_null_and_small_workspace():
+    lib = _lib.load()
+    w = _lib.G2KWeights(*([ctypes.c_void_p(16)] * 7))
+    p = ctypes.c_void_p(16)
+    rc = lib.g2k_step_fused_f32(ctypes.byref(_dims()), ctypes.byref(w), None, p, p, p, p, None,
+                                None, p, p, p, p, None, None, 5e-4, p, 1 << 30, None)
+    assert rc == -1
+    need = lib.g2k_step_workspace_bytes(ctypes.byref(_dims()))
+    assert need == 2 * 20 * 256 * 4 + 2 * 5 * 8 * 4
+    rc = lib.g2k_step_fused_f32(ctypes.byref(_dims()), ctypes.byref(w), p, p, p, p, p, None,
+                                None, p, p, p, p, None, None, 5e-4, p, need - 4, None)
+    assert rc == -1 and b"workspace" in lib.g2k_last_error()
+
+
+def test_other_entry_points_validate():
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)
+    assert lib.g2k_frame_recurrence_f32(ctypes.byref(_dims(H=100)), p, p, 3, None) == -4
+    assert lib.g2k_ade_fde_f32(ctypes.byref(_dims(L=10)), p, p, p, None, None, 0, p, None) == -4
+    assert lib.g2k_ade_fde_f32(ctypes.byref(_dims()), p, p, p, None, None, 7, p, None) == -1
+    assert lib.g2k_infer_rlns_f32(None, p, 4, 4, None) == -1
+    assert lib.g2k_eval_rln_ngh_f32(p, p, 4, 0, None) == -1
+    assert lib.g2k_step_lds_bytes(ctypes.byref(_dims(T=9))) == 0
+
+
+def test_zero_scenes_is_a_noop():
+    lib = _lib.load()
+    w = _lib.G2KWeights(*([ctypes.c_void_p(16)] * 7))
+    p = ctypes.c_void_p(16)
+    rc = lib.g2k_step_fused_f32(ctypes.byref(_dims(S=0)), ctypes.byref(w), p, p, p, p, p, None,
+                                None, p, p, p, p, None, None, 5e-4, p, 0, None)
+    assert rc == 0

@@ -1,0 +1,76 @@
+"""world_size-2 gloo test of the data-parallel path on CPU: each rank runs its
+shard of scenes (the float64 oracle stands in for the GPU step here) and the
+all-reduced metric sums equal the single-process sums."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from multimodaltraj_2_amd.dist import global_errors, reduce_metrics, shard_scenes
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _scene_metrics(S, lo, hi):
+    from multimodaltraj_2_amd.synthetic import make_batch
+    from oracle import g2k_ref as ref
+    b = make_batch(S, 16, 64, F=4, seed=11)
+    rng = np.random.default_rng(0)
+    shapes = dict(Wi=(16, 16), Wii=(16, 8), Wv=(8, 18), bv=(16,), Wr=(8, 2), Wc=(24, 8), Wo=(8, 16))
+    w = {k: rng.standard_normal(s) for k, s in shapes.items()}
+    rows = []
+    for s in range(lo, hi):
+        _, _, m, _ = ref.scene_step(b.pos[s], b.vislet[s], b.G[s], w, b.targets[s], b.n_active[s],
+                                    b.h0[s], n_frames=b.F)
+        rows.append(m)
+    return torch.tensor(np.array(rows), dtype=torch.float64).reshape(-1, 8)
+
+
+def _worker(rank, world, port, S, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_scenes(S, rank, world)
+    tot = reduce_metrics(_scene_metrics(S, lo, hi))
+    if rank == 0:
+        q.put(tot.numpy())
+    dist.destroy_process_group()
+
+
+def test_shard_scenes_partition():
+    for total in (0, 1, 7, 256, 1023):
+        for world in (1, 2, 3, 8):
+            spans = [shard_scenes(total, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_scenes(4, 2, 2)
+
+
+def test_two_rank_gloo_metric_reduction():
+    S, world = 6, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, S, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = _scene_metrics(S, 0, S).sum(dim=0).numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-12)
+    ade, fde = global_errors(torch.tensor(got))
+    assert np.isfinite(ade) and np.isfinite(fde)

@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Runs only in the build container, where /root/reference exists (no-op
+elsewhere).  It imports the reference's own data-side modules
+(load_traj.py, networkx_graph.py, argParser.py — numpy/networkx/torch only)
+and records their outputs for the first batches of each dataset:
+
+  * DataLoader.load_dataset (load_traj.py:114-150) on the dataset CSV,
+  * the frame dict of DataLoader.frame_preprocess (load_traj.py:234-256),
+    restated here because the reference only returns it through a pickle
+    file (it is rebuilt from the CSV: trajectories_0.cpkl is never unpickled),
+  * DataLoader.next_step (load_traj.py:153-224) — batches and targets,
+  * online_graph.ConstructGraph + get_node_attr (networkx_graph.py:30-73,
+    114-150) as called by train.py:74-90 / 280-299 (float frame key cast to
+    int, quirk Q9) and by sample.py:150-164 (fresh graph, framenum 0),
+  * the batch_v preprocessing of train.py:76-85 and sample.py:152-164.
+
+Writes tests/golden/data_<name>.npz (inputs and expected outputs; data only).
+
+Also decodes the TF tensor-bundle checkpoint
+save/g2k_mcrAttn_model_kfold_train_4_0.ckpt-79 (.index SSTable of
+BundleEntryProto + raw .data) and stores, for every model copy, weight_c,
+cost and the forward Variable holding weight_c @ cost (models/g2k_lstm_mcr.py:122)
+as tests/golden/ckpt_mcr_attn.npz — a known-answer test for the oracle.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import struct
+import sys
+
+import numpy as np
+
+REF = "/root/reference"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tests", "golden")
+
+DATASETS = {  # name -> (dir relative to data/, csv selection index 0)
+    "eth_hotel": "eth/hotel/",
+    "zara01": "ucy/zara/zara01/",
+    "zara02": "ucy/zara/zara02/",
+    "ucy_univ": "ucy/univ/",
+}
+N_BATCHES = 3
+
+
+def frame_dict_from_csv(dl):
+    """load_traj.py:234-256 restated (the reference writes it to a pickle)."""
+    frame_data = {i: {} for i in dl.frameList}
+    ppfl = np.transpose(dl.pedsPerFrameList)
+    fp = dl.frame_pointer
+    while fp <= max(dl.frameList):
+        frame_data[fp] = [{ped: [px, py]} for (ind, ped, px, py) in ppfl if ind == fp]
+        fp += dl.diff
+    return frame_data
+
+
+def make_data_fixture(name, rel):
+    sys.path.insert(0, REF)
+    import argParser
+    import load_traj
+    import networkx_graph
+
+    args = argParser.ArgsParser().parser.parse_args([])
+    d = os.path.join(REF, "data", rel)
+    csv = sorted(glob.glob(d + "*.csv"))[0]
+    dl = load_traj.DataLoader.__new__(load_traj.DataLoader)
+    dl.batch_size, dl.seq_length = args.batch_size, args.seq_length
+    dl.pred_len, dl.obs_len, dl.diff = args.pred_len, args.obs_len, args.obs_len
+    dl.infer = False
+    dl.current_dir = d
+    dl.load_dataset(csv)
+    dl.trajectories = frame_dict_from_csv(dl)
+    dl.num_batches = int((len(dl.frameList) / dl.seq_length) / dl.batch_size)
+    dl.reset_data_pointer()
+    graph = networkx_graph.online_graph(args)
+
+    # next_step's `targets={}` default is one dict shared by every call in the
+    # process (load_traj.py:153): start each dataset's fixture from empty
+    load_traj.DataLoader.next_step.__defaults__[0].clear()
+    rec = {"raw_data": dl.raw_data, "num_batches": np.int64(dl.num_batches)}
+    frame = 1                                  # train.py:34
+    for b in range(N_BATCHES):
+        batch, target_traj, fptr = dl.next_step()
+        keys = np.array(list(batch.keys()), dtype=np.float64)
+        # the frame dicts of this batch, flattened: (frame key, ped id, x, y)
+        flat = [(k, float(ped), pos[0], pos[1]) for k in batch for item in batch[k]
+                for ped, pos in item.items()]
+        rec[f"b{b}_keys"] = keys
+        rec[f"b{b}_frames_flat"] = np.array(flat, dtype=np.float64).reshape(-1, 4)
+        rec[f"b{b}_frame_pointer"] = np.float64(fptr)
+        tkeys = list(target_traj.keys())
+        rec[f"b{b}_target_ids"] = np.array(tkeys, dtype=np.int64)
+        rec[f"b{b}_target_lens"] = np.array([len(target_traj[k]) for k in tkeys], dtype=np.int64)
+        rec[f"b{b}_target_flat"] = (np.concatenate([np.asarray(target_traj[k], dtype=np.float64)
+                                                    for k in tkeys]).reshape(-1, 2)
+                                    if tkeys else np.zeros((0, 2)))
+        # train.py path (stateful graph; framenum = previous frame key, cast to int: Q9)
+        g = graph.ConstructGraph(current_batch=batch, framenum=int(frame), future_traj=target_traj)
+        npl = g.get_node_attr(param="node_pos_list")
+        rec[f"b{b}_node_ids"] = np.array(list(npl.keys()), dtype=np.int64)
+        rec[f"b{b}_node_pos_list"] = np.array(list(npl.values()), dtype=np.float64).reshape(-1, 8, 2)
+        bv = np.array(list(npl.values()))
+        if len(bv.shape) > 1:
+            bv = np.linalg.norm(np.array(bv)[int(frame):int(frame) + args.obs_len], axis=2).squeeze()
+            bv = np.transpose(bv)
+        rec[f"b{b}_batch_v_train"] = np.asarray(bv, dtype=np.float64)
+        rec[f"b{b}_framenum"] = np.int64(int(frame))
+        # sample.py path: fresh graph each batch, framenum 0, time slice
+        gs = networkx_graph.online_graph(args).ConstructGraph(current_batch=batch, framenum=0,
+                                                              future_traj=target_traj)
+        npl_s = np.array(list(gs.get_node_attr(param="node_pos_list").values()))
+        bvs = np.transpose(np.linalg.norm(npl_s[:, 0:args.obs_len], axis=2))
+        rec[f"b{b}_batch_v_sample"] = bvs.astype(np.float64)
+        tg = gs.get_node_attr(param="targets")
+        rec[f"b{b}_sample_target_ids"] = np.array(list(tg.keys()), dtype=np.int64)
+        rec[f"b{b}_sample_target_lens"] = np.array([len(v[0]) for v in tg.values()], dtype=np.int64)
+        rec[f"b{b}_sample_targets_flat"] = (np.concatenate([np.asarray(v[0], dtype=np.float64).reshape(-1, 2)
+                                                             for v in tg.values()])
+                                            if tg else np.zeros((0, 2)))
+        for k in batch:                        # train.py:197 leaves `frame` at the last key
+            frame = k
+    np.savez_compressed(os.path.join(OUT, f"data_{name}.npz"), **rec)
+    return rec
+
+
+# ---------------------------------------------------------------------------
+# TF tensor bundle (.index = LevelDB-style table of BundleEntryProto)
+# ---------------------------------------------------------------------------
+def _varint(b, i):
+    r = s = 0
+    while True:
+        c = b[i]; i += 1
+        r |= (c & 0x7F) << s; s += 7
+        if c < 0x80:
+            return r, i
+
+
+def _block_entries(buf):
+    nrest = struct.unpack_from("<I", buf, len(buf) - 4)[0]
+    end = len(buf) - 4 - 4 * nrest
+    i, key, out = 0, b"", []
+    while i < end:
+        shared, i = _varint(buf, i)
+        nonshared, i = _varint(buf, i)
+        vlen, i = _varint(buf, i)
+        key = key[:shared] + buf[i:i + nonshared]; i += nonshared
+        out.append((key, buf[i:i + vlen])); i += vlen
+    return out
+
+
+def _proto_fields(b):
+    i, out = 0, {}
+    while i < len(b):
+        tag, i = _varint(b, i)
+        f, wt = tag >> 3, tag & 7
+        if wt == 0:
+            v, i = _varint(b, i)
+        elif wt == 2:
+            n, i = _varint(b, i); v = b[i:i + n]; i += n
+        elif wt == 5:
+            v = b[i:i + 4]; i += 4
+        elif wt == 1:
+            v = b[i:i + 8]; i += 8
+        else:
+            raise ValueError("wire type")
+        out.setdefault(f, []).append(v)
+    return out
+
+
+def read_bundle(prefix):
+    idx = open(prefix + ".index", "rb").read()
+    data = open(prefix + ".data-00000-of-00001", "rb").read()
+    footer = idx[-48:]
+    _, j = _varint(footer, 0); _, j = _varint(footer, j)      # metaindex handle
+    ioff, j = _varint(footer, j); isz, j = _varint(footer, j)  # index handle
+    tensors = {}
+    for _, handle in _block_entries(idx[ioff:ioff + isz]):
+        off, k = _varint(handle, 0); sz, k = _varint(handle, k)
+        for key, val in _block_entries(idx[off:off + sz]):
+            if not key:
+                continue                               # header entry
+            fl = _proto_fields(val)
+            dtype = fl.get(1, [0])[0]
+            shape = [_proto_fields(d).get(1, [0])[0]
+                     for d in _proto_fields(fl[2][0]).get(2, [])] if 2 in fl else []
+            o = fl.get(4, [0])[0]; n = fl.get(5, [0])[0]
+            if dtype == 2:                             # DT_DOUBLE
+                tensors[key.decode()] = np.frombuffer(data[o:o + n], dtype="<f8").reshape(shape)
+    return tensors
+
+
+def make_ckpt_fixture():
+    """Known answers from the reference's own checkpoints.
+
+    mcrAttn: the forward Variable [24, 8] created at models/g2k_lstm_mcr.py:122
+    equals weight_c @ (the forward cost Variable [8, 8] of :112) for the
+    model copies whose variables were initialised in one run (5 of 20).
+    mc: g2k_lstm_mc's forward Variables [24, 8] / [24, 304] are all zero
+    (cost = d placeholder / d Variable = 0, models/g2k_lstm_mc.py:59-66)."""
+    t = read_bundle(os.path.join(REF, "save", "g2k_mcrAttn_model_kfold_train_4_0.ckpt-79"))
+    out = {}
+    wcs = {k: v for k, v in sorted(t.items()) if k.endswith("/weight_c")}
+    c88 = {k: v for k, v in t.items() if k.startswith("Variable") and v.shape == (8, 8)}
+    fwd = {k: v for k, v in t.items() if k.startswith("Variable") and v.shape == (24, 8)}
+    n = 0
+    for gk, wc in wcs.items():
+        for ck, c in c88.items():
+            prod = wc @ c
+            for k, v in fwd.items():
+                if np.abs(v - prod).max() <= 1e-15 * max(1.0, np.abs(v).max()):
+                    out[f"pair{n}_weight_c"], out[f"pair{n}_cost"], out[f"pair{n}_temp"] = wc, c, v
+                    out[f"pair{n}_names"] = np.array([gk, ck, k])
+                    n += 1
+    out["n_pairs"] = np.int64(n)
+    tm = read_bundle(os.path.join(REF, "save", "g2k_mc_model_kfold_train_4_0.ckpt-79"))
+    g = sorted(k for k in tm if k.endswith("/weight_c"))[0].rsplit("/", 1)[0]
+    out["mc_weight_c"] = tm[g + "/weight_c"]
+    out["mc_weight_o"] = tm[g + "/weight_o"]
+    zeros = [k for k, v in tm.items() if k.startswith("Variable") and v.shape in ((24, 8), (24, 304))]
+    out["mc_forward_all_zero"] = np.array([bool(np.all(tm[k] == 0)) for k in zeros])
+    np.savez_compressed(os.path.join(OUT, "ckpt_mcr_attn.npz"), **out)
+    return n, len(t)
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("no /root/reference here: fixtures are committed, nothing to do")
+        return
+    os.makedirs(OUT, exist_ok=True)
+    for name, rel in DATASETS.items():
+        rec = make_data_fixture(name, rel)
+        print(name, {k: np.shape(v) for k, v in rec.items() if k.startswith("b0")})
+    print("checkpoint pairs (weight_c @ cost == stored Variable):", make_ckpt_fixture())
+
+
+if __name__ == "__main__":
+    main()
