@@ -1,0 +1,39 @@
+"""Flags of the reference (argParser.py:3-73), same names and defaults, plus
+the build's own: --data_root (Q8), --device, --slice, --chain_hidden,
+--log_dir, --seed."""
+import argparse
+
+
+class ArgsParser:
+    parser = argparse.ArgumentParser()
+    parser.add_argument('--input_size', type=int, default=2)
+    parser.add_argument('--rnn_size', type=int, default=128)
+    parser.add_argument('--num_layers', type=int, default=2)
+    parser.add_argument('--model', type=str, default='lstm')
+    parser.add_argument('--batch_size', type=int, default=16)
+    parser.add_argument('--seq_length', type=int, default=12)
+    parser.add_argument('--pred_len', type=int, default=12)
+    parser.add_argument('--obs_len', type=int, default=8)
+    parser.add_argument('--num_epochs', type=int, default=10)
+    parser.add_argument('--save_every', type=int, default=50)
+    parser.add_argument('--grad_clip', type=float, default=10.)
+    parser.add_argument('--learning_rate', type=float, default=0.005)
+    parser.add_argument('--decay_rate', type=float, default=0.95)
+    parser.add_argument('--dropout', type=float, default=0.8)
+    parser.add_argument('--embedding_size', type=int, default=64)
+    parser.add_argument('--neighborhood_size', type=int, default=64)
+    parser.add_argument('--grid_size', type=int, default=4)
+    parser.add_argument('--num_freq_blocks', type=int, default=10)
+    parser.add_argument('--maxNumPeds', type=int, default=20)
+    parser.add_argument('--leaveDataset', type=int, default=2)
+    parser.add_argument('--lambda_param', type=float, default=0.0005)
+    # build additions
+    parser.add_argument('--data_root', type=str, default='data',
+                        help='directory holding eth/ and ucy/ (replaces hard-coded paths, Q8)')
+    parser.add_argument('--device', type=str, default='cuda')
+    parser.add_argument('--slice', choices=('train', 'sample'), default='train',
+                        help="batch_v slice: train.py node slice (Q10) or sample.py time slice")
+    parser.add_argument('--chain_hidden', type=int, default=1,
+                        help='carry hidden_state from batch to batch like train.py')
+    parser.add_argument('--log_dir', type=str, default='log')
+    parser.add_argument('--seed', type=int, default=0)

@@ -1096,12 +1096,13 @@ StepPlan plan_step(const g2k_dims* d) {
   return p;
 }
 
-// Waves per recurrence workgroup: 8 (two per SIMD, so one wave's latency
-// hides under the other's issue) whenever H allows 16-column tiles per wave.
+// Waves per recurrence workgroup: 4 (one per SIMD).  8 waves (two per SIMD)
+// measured 0-5 % slower at H = 128 / 256 (tools/tune_recur.py); kept as a
+// tuning option.
 int recur_waves(int H) {
   const char* env = getenv("G2K_RECUR_WAVES");   // tuning override (4 or 8)
   if (env && (atoi(env) == 4 || (atoi(env) == 8 && H >= 128))) return atoi(env);
-  return H >= 128 ? 8 : 4;
+  return 4;
 }
 
 int launch_recur(const RecurArgs& r, int S, hipStream_t st) {

@@ -1,0 +1,100 @@
+"""GPU: the reference-signature classes and the real-data plumbing (config 1)
+through the C ABI vs the float64 oracle.  Tolerance |d| <= 1e-4*max(1,|ref|)."""
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from multimodaltraj_2_amd import frame_step as fs
+from multimodaltraj_2_amd import networkx_graph as nxg
+from multimodaltraj_2_amd import nri_learned
+from multimodaltraj_2_amd.load_traj import DataLoader
+from multimodaltraj_2_amd.models.g2k_lstm_mcr import g2k_lstm_mcr
+from multimodaltraj_2_amd.models.gsk_lstm_cell import gsk_lstm_cell
+from multimodaltraj_2_amd.scenes import build_scene, pack
+from oracle import g2k_ref as ref
+from tests.conftest import close
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+ARGS = SimpleNamespace(batch_size=16, seq_length=12, pred_len=12, obs_len=8)
+
+
+def test_g2k_lstm_mcr_class_forward(gpu):
+    m = g2k_lstm_mcr(in_features=torch.zeros(16, 16), hidden_size=128, obs_len=8, num_nodes=7,
+                     lambda_reg=5e-4, sess_g=None, device=gpu)
+    rng = np.random.default_rng(5)
+    feed = dict(outputs=rng.standard_normal((18, 16)), ngh=rng.standard_normal((16, 8)),
+                rel_features=rng.standard_normal((2, 16)) ** 2, out_size=7)
+    pred = m.forward(feed).cpu().numpy()
+    o = ref.mcr_forward(feed["outputs"].astype(np.float32), feed["rel_features"].astype(np.float32),
+                        feed["ngh"].astype(np.float32), m.weight_v.cpu().numpy(),
+                        m.bias_v.cpu().numpy(), m.weight_r.cpu().numpy(), m.weight_c.cpu().numpy(),
+                        m.weight_o.cpu().numpy(), 5e-4)
+    assert pred.shape == (2, 12, 7)
+    assert close(pred, o["pred_path_band"]) <= TOL
+    assert close(m.cost.cpu().numpy(), o["cost"]) <= TOL
+    assert close(m.attn.cpu().numpy(), o["attn"]) <= TOL
+
+
+def test_gsk_lstm_cell_fails_like_reference(gpu):
+    with pytest.raises(ValueError):
+        gsk_lstm_cell(torch.zeros(16, 16), 16, 8, 5, 5e-4, device=gpu)
+    with pytest.raises(ValueError):
+        gsk_lstm_cell(torch.zeros(16, 16), 16, 12, 5, 5e-4, device=gpu)
+    c = gsk_lstm_cell(torch.zeros(16, 16), 16, 12, 0, 5e-4, device=gpu)
+    assert tuple(c.pred_path_band.shape) == (2, 12, 0)
+
+
+def test_nri_ops(gpu):
+    rng = np.random.default_rng(6)
+    adj = rng.standard_normal((5, 16, 16)).astype(np.float32) * 4
+    t = torch.from_numpy(adj).to(gpu)
+    assert close(nri_learned.infer_rlns(t).cpu().numpy(), ref.infer_rlns(adj)) <= TOL
+    assert close(nri_learned.eval_rln_ngh(t).cpu().numpy(), ref.eval_rln_ngh(adj)) <= TOL
+
+
+@pytest.mark.parametrize("name", ["zara01", "ucy_univ", "eth_hotel"])
+@pytest.mark.parametrize("mode", ["train", "sample"])
+def test_real_data_plumbing(gpu, name, mode):
+    """Config 1: DataLoader -> online graph -> scene tensors -> HIP step, per
+    batch with the hidden state carried over (train.py), vs the oracle."""
+    z = np.load(os.path.join(GOLDEN, f"data_{name}.npz"))
+    dl = DataLoader(ARGS, raw_data=z["raw_data"])
+    dl.reset_data_pointer()
+    graph = nxg.online_graph(ARGS)
+    frame = 1
+    scenes = []
+    for b in range(3):
+        batch, tgt, _ = dl.next_step()
+        g = (graph.ConstructGraph(batch, tgt, int(frame)) if mode == "train" else
+             nxg.online_graph(ARGS).ConstructGraph(batch, tgt, 0))
+        sc = build_scene(batch, tgt, g, dl, frame, mode=mode)
+        for k in batch:
+            frame = k
+        if sc.window.shape[1] >= 2:
+            scenes.append(sc)
+    assert scenes
+    pk = pack(scenes, 128)
+    S, Nmax, F = len(scenes), pk["Nmax"], pk["F"]
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    t = {k: torch.from_numpy(v).to(gpu) for k, v in pk.items() if isinstance(v, np.ndarray)}
+    G = torch.from_numpy(np.random.default_rng(1).standard_normal((S, 16, 8)).astype(np.float32)).to(gpu)
+    h0 = torch.zeros((S, 16, 128), device=gpu)
+    out = fs.step_fused(params, t["pos"], t["vislet"], G, t["targets"], t["n_active"], h0,
+                        n_frames=t["n_frames"], ped_mask=t["ped_mask"], stride=0)
+    torch.cuda.synchronize()
+    w = params.numpy()
+    for s in range(S):
+        n = int(pk["n_active"][s])
+        pr, h, m, _ = ref.scene_step(pk["pos"][s], pk["vislet"][s], G[s].cpu().numpy(), w,
+                                     pk["targets"][s], n, np.zeros((16, 128)),
+                                     n_frames=int(pk["n_frames"][s]), stride=0,
+                                     ped_mask=pk["ped_mask"][s].astype(bool))
+        nf = pr.shape[0]
+        assert close(out.pred[s, :nf, :, :n].cpu().numpy().reshape(nf, 2, 12, n), pr) <= TOL
+        assert close(out.h[s].cpu().numpy(), h) <= TOL
+        assert close(out.metrics[s, :6].cpu().numpy(), m[:6]) <= TOL
