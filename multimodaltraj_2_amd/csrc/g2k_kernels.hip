@@ -52,6 +52,7 @@ int check_launch(const char* what) {
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 #ifdef G2K_STAMPS
 // diagnostic build only: s_memtime stamps of workgroup 0 of each kernel
@@ -65,29 +66,24 @@ __device__ unsigned long long g2k_stamps[64];
 #define STAMP(k) do {} while (0)
 #endif
 
-#ifdef G2K_STAMPS_RECUR
-// diagnostic build only: in-frame stamps of wave 0 of workgroup 0, frame 5
-__device__ unsigned long long g2k_rstamps[16];
-__device__ int g2k_rframe;
-#define RSTAMP(k)                                                             \
-  do {                                                                        \
-    unsigned long long _t;                                                    \
-    __builtin_amdgcn_sched_barrier(0);                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory"); \
-    __builtin_amdgcn_sched_barrier(0);                                        \
-    if (blockIdx.x == 0 && threadIdx.x == 0 && g2k_rframe == 5) g2k_rstamps[(k)] = _t; \
+#ifdef G2K_STAMPS_SCENE
+// diagnostic build only: timeline of scene-kernel workgroups 0, 85, 170, 255
+__device__ unsigned long long g2k_sstamps[4][128];
+#define SSTAMP(k, cond)                                                         \
+  do {                                                                          \
+    if ((cond) && (blockIdx.x % 85) == 0 && blockIdx.x < 340) {                 \
+      unsigned long long _t;                                                    \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory"); \
+      g2k_sstamps[blockIdx.x / 85][(k)] = _t;                                   \
+    }                                                                           \
   } while (0)
 #else
-#define RSTAMP(k) do {} while (0)
+#define SSTAMP(k, cond) do {} while (0)
 #endif
+
 
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
-// Diagnostic ablation switches for tools/ablate_recur.py (never set in the
-// shipped build; every switch breaks the results on purpose).
-#ifndef G2K_ABL
-#define G2K_ABL 0
-#endif
 
 // LDS-DMA: 16 bytes per lane, LDS destination = wave-uniform base + 16*lane.
 __device__ __forceinline__ void dma16(const float* gsrc, float* lds_wave_base) {
@@ -107,6 +103,15 @@ __device__ __forceinline__ void dma_copy_n(const float* g, float* lds, int n4, i
 
 // Copy n floats global -> LDS with the whole workgroup by 4-byte LDS-DMA
 // (no alignment requirement beyond 4 bytes); caller waits vmcnt(0) + barrier.
+template <int NT>
+__device__ __forceinline__ void dma4_copy_t(const float* g, float* lds, int n, int wv, int lane) {
+  for (int i = wv * 64; i < n; i += NT) {
+    if (i + lane < n)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + i + lane),
+                                       (__attribute__((address_space(3))) void*)(lds + i), 4, 0, 0);
+  }
+}
+
 __device__ __forceinline__ void dma4_copy(const float* g, float* lds, int n, int wv, int lane) {
   for (int i = wv * 64; i < n; i += kNT) {
     if (i + lane < n)
@@ -132,17 +137,36 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
-__device__ __forceinline__ float row16_max(float v) {
-  v = fmaxf(v, dpp<0xB1>(v));
-  v = fmaxf(v, dpp<0x4E>(v));
-  v = fmaxf(v, dpp<0x141>(v));
-  v = fmaxf(v, dpp<0x140>(v));
-  return v;
+
+// Sum over the four 16-lane rows of a wave (lanes r, r+16, r+32, r+48),
+// identical bits in all four lanes: v_permlane32_swap + v_permlane16_swap.
+__device__ __forceinline__ float sum_rows4(float v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
+// Sum over all 64 lanes (DPP + permlane, no LDS); every lane gets the result.
+__device__ __forceinline__ float wave_sum(float v) { return sum_rows4(row16_sum(v)); }
+
+// Four per-lane values v[i] (rows 4q + i of an MFMA result, this lane's
+// column) reduced over the 16 lanes of each lane group by a transposing
+// butterfly: 2 + 1 DPP exchanges hand each lane one row, 2 more finish the
+// row.  Lane L ends with the reduction of row 4q + reduce4_row(L).
+__device__ __forceinline__ int reduce4_row(int L) { return 2 * (L & 1) + ((L >> 1) & 1); }
+
+template <bool MAX>
+__device__ __forceinline__ float reduce4_rows16(float v0, float v1, float v2, float v3, int L) {
+  auto op = [](float x, float y) { return MAX ? fmaxf(x, y) : x + y; };
+  const bool odd = (L & 1) != 0, b1 = (L & 2) != 0;
+  const float s0 = odd ? v0 : v2, s1 = odd ? v1 : v3;        // rows the xor-1 partner keeps
+  const float a0 = op(odd ? v2 : v0, dpp<0xB1>(s0));        // quad_perm [1,0,3,2]
+  const float a1 = op(odd ? v3 : v1, dpp<0xB1>(s1));
+  float r = op(b1 ? a1 : a0, dpp<0x4E>(b1 ? a0 : a1));      // quad_perm [2,3,0,1]
+  r = op(r, dpp<0x124>(r));                                 // row_ror:4
+  r = op(r, dpp<0x128>(r));                                 // row_ror:8
+  return r;
 }
 
 // ---------------------------------------------------------------------------
@@ -223,196 +247,234 @@ __device__ __forceinline__ void attn_row_pass(float* A, int r, float* gout) {
   }
 }
 
-// Sum / max over the four 16-lane rows of a wave (lanes r, r+16, r+32, r+48),
-// identical bits in all four lanes: v_permlane32_swap + v_permlane16_swap.
-__device__ __forceinline__ float sum_rows4(float v) {
-  if (G2K_ABL & 1) return v;
-  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+
+// ---------------------------------------------------------------------------
+// LDS polling for the wave-specialised scene kernel.  The loads are inline
+// asm (the compiler may neither hoist nor merge them) and wait for their own
+// data; LDS services one CU's requests in order, so a flag read that sees a
+// producer's flag write is followed by data reads that see the data the
+// producer wrote before it (the producer waits lgkmcnt(0) between the two).
+// A poll gives up after kPollMax rounds (~50 ms) so that a broken invariant
+// yields wrong numbers, not a hung GPU.
+// ---------------------------------------------------------------------------
+constexpr int kPollMax = 1 << 20;
+#ifndef G2K_POLL_SLEEP
+#define G2K_POLL_SLEEP 1
+#endif
+
+__device__ __forceinline__ void poll_pause() {
+  if (G2K_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(G2K_POLL_SLEEP);
 }
 
-__device__ __forceinline__ float max_rows4(float v) {
-  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+
+
+// One frame's inputs of the recurrence in one LDS round trip: the 4
+// recurrence waves' sequence words (seq[w] = frames whose row partials wave w
+// has published, +1), the producer's flag of this frame's As tile, the As row
+// quad and the row partials of the 4 waves.  Each writer stores its data
+// before its word, and the words are read before the data, so seeing
+// min(seq) >= want_seq and flag == want_flag means the data read is current.
+// Busy poll for the first rounds (the scene's critical path), then s_sleep.
+__device__ __forceinline__ void poll_frame(const int* seq, int want_seq, const int* flag,
+                                           int want_flag, const float* asrc, const float* rsrc,
+                                           float4& b, float4& z) {
+  const uint32_t sa = lds_addr(seq), fa = lds_addr(flag), da = lds_addr(asrc), ra = lds_addr(rsrc);
+  int fl;
+  i32x4 sq;
+  f32x4 v, a0, a1, a2, a3;
+  for (int it = 0; it < kPollMax; ++it) {
+    asm volatile(
+        "ds_read_b128 %0, %7\n\t"
+        "ds_read_b32 %1, %8\n\t"
+        "ds_read_b128 %2, %9\n\t"
+        "ds_read_b128 %3, %10\n\t"
+        "ds_read_b128 %4, %10 offset:64\n\t"
+        "ds_read_b128 %5, %10 offset:128\n\t"
+        "ds_read_b128 %6, %10 offset:192\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(sq), "=&v"(fl), "=&v"(v), "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+        : "v"(sa), "v"(fa), "v"(da), "v"(ra)
+        : "memory");
+    const int smin = min(min(__builtin_amdgcn_readfirstlane(sq[0]), __builtin_amdgcn_readfirstlane(sq[1])),
+                         min(__builtin_amdgcn_readfirstlane(sq[2]), __builtin_amdgcn_readfirstlane(sq[3])));
+    if (smin >= want_seq && __builtin_amdgcn_readfirstlane(fl) == want_flag) break;
+    if (it >= 8) __builtin_amdgcn_s_sleep(1);   // long waits (the first heads): back off
+  }
+  b = make_float4(v[0], v[1], v[2], v[3]);
+  z = make_float4(((a0[0] + a1[0]) + a2[0]) + a3[0], ((a0[1] + a1[1]) + a2[1]) + a3[1],
+                  ((a0[2] + a1[2]) + a2[2]) + a3[2], ((a0[3] + a1[3]) + a2[3]) + a3[3]);
+}
+
+// Wait until a frame flag reaches `want` (no data attached).
+__device__ __forceinline__ void poll_flag(const int* flag, int want) {
+  const uint32_t fa = lds_addr(flag);
+  int fl;
+  for (int it = 0; it < kPollMax; ++it) {
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(fl) : "v"(fa) : "memory");
+    if (__builtin_amdgcn_readfirstlane(fl) == want) break;
+    poll_pause();
+  }
 }
 
 // ---------------------------------------------------------------------------
 // Hidden recurrence (train.py:243-252), h in registers:
 //   h <- softmax(h, -1); h <- As @ h; adj <- softmax(h, -1) @ 1; h <- adj * h
-// computed as h'^T = e^T @ (diag(1/Z) As^T) with v_mfma_f32_16x16x4_f32
-// (M = 16 columns of h, N = the 16 rows, K = 16 in four k-steps), where
-// e = exp(h) and Z its row sums (softmax = e / Z).  Wave w owns columns
-// [w*H/4, (w+1)*H/4) as TPW 16-wide tiles; lane l (r = l & 15, q = l >> 4)
-// holds ONE row r: h'[r][16t + 4q + i] in x[t][i].
+// computed as h' = (As diag(1/Z)) @ e with v_mfma_f32_16x16x4_f32 (M = the 16
+// rows, N = 16 columns per tile, K = 16 in four k-steps), e = exp(h) and Z its
+// row sums (softmax = e / Z).  Wave w owns columns [w*H/NW, (w+1)*H/NW) as TPW
+// 16-wide tiles; lane (L = lane & 15, q = lane >> 4) holds rows 4q..4q+3 of
+// column 16t + L: h'[4q + i][16t + L] in x[t][i].  That is the MFMA result
+// layout and also exactly the B operand of the next frame's product
+// (register ks = e[4q + ks][c]), so nothing is transposed between frames.  The
+// A operand of lane (L, q) at k-step ks is As[L][4q + ks] / Z_{4q+ks}: one
+// float4 of the As tile times the reciprocal row sums of the lane's own rows.
 //
-// Per frame: (1) e goes through a wave-local 16x16 transpose in LDS into the
-// A-operand layout (no barrier); (2) the row sums Z_k of rows k = 4q..4q+3,
-// published by all four waves at the previous exchange, scale the B operand
-// As[r][k] / Z_k; (3) four MFMA k-steps per tile; (4) e2 = exp(h'), its per-row
-// partial sum (local + 2 permlane steps) is published for the next frame:
-// ONE 4-wave LDS exchange (one barrier) per frame.
+// Per frame: four MFMA k-steps per tile; e = exp(h'); per-row partial sums
+// over the wave's columns (local + 16-lane DPP) published as one float4 per
+// lane group; ONE NW-wave LDS exchange per frame (a workgroup barrier in
+// g2k_recur_kernel, flag polling in the fused scene kernel).
 //
 // adj = sum_j softmax(h')_rj is evaluated from the published partials
 // (sum_w P_w / Z) and scales the final h.  The next frame's softmax needs
 // exp(adj * h'); |adj - 1| <= a few ulp (adj == 1 exactly in real arithmetic)
 // and h' lies in [0, 1] (convex combinations of softmax outputs), so in fp32
 // adj * h' is within one ulp of h' and exp(adj * h') is evaluated as
-// exp(h') = e2 (DESIGN.md "recurrence numerics"); the same bound makes the
+// exp(h') = e (DESIGN.md "recurrence numerics"); the same bound makes the
 // tf.nn.softmax max shift the identity after frame 0.
 // ---------------------------------------------------------------------------
-constexpr int kTP = 20;            // transpose tile row pitch (floats): conflict-free b32 reads
-constexpr int kTTile = kD * kTP;   // 320 floats per 16x16 tile
-
 template <int TPW, int NW>
 struct Recur {
   static constexpr int kCols = 16 * TPW;   // columns per wave (H = NW * kCols)
   float x[TPW][4];    // h (before init) / the last h' (after a step)
-  float e[TPW][4];    // numerators of the next softmax(h), row r
-  float av[TPW][4];   // e transposed into the A-operand layout: e[4q + ks][16t + r]
+  float e[TPW][4];    // exp(h'): numerators of the next softmax(h) = next B operand
 
-  __device__ __forceinline__ void load(const float* __restrict__ hs, int H, int wv, int q, int r) {
+  __device__ __forceinline__ void load(const float* __restrict__ hs, int H, int wv, int q, int L) {
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      const float4 v = *reinterpret_cast<const float4*>(hs + r * H + wv * kCols + 16 * t + 4 * q);
-      x[t][0] = v.x; x[t][1] = v.y; x[t][2] = v.z; x[t][3] = v.w;
-    }
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[t][i] = hs[(4 * q + i) * H + wv * kCols + 16 * t + L];
   }
 
   // h = adj * h' with adj = row sum of softmax(h') from the last exchange
-  // (red: that frame's [4 waves][16 rows] partials), or h unchanged (nf == 0).
-  __device__ __forceinline__ void store(float* __restrict__ hs, int H, int wv, int q, int r,
+  // (red: that frame's [NW waves][16 rows] partials), or h unchanged (red NULL).
+  __device__ __forceinline__ void store(float* __restrict__ hs, int H, int wv, int q, int L,
                                         const float* red) const {
-    float adj = 1.0f;
+    float adj[4] = {1.f, 1.f, 1.f, 1.f};
     if (red) {
-      float z = 0.f;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) z += red[16 * w + r];
-      const float rz = rcp(z);
-      adj = 0.f;
+      for (int i = 0; i < 4; ++i) {
+        float z = 0.f;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) adj = fmaf(red[16 * w + r], rz, adj);
+        for (int w = 0; w < NW; ++w) z += red[16 * w + 4 * q + i];
+        const float rz = rcp(z);
+        adj[i] = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) adj[i] = fmaf(red[16 * w + 4 * q + i], rz, adj[i]);
+      }
     }
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
-      *reinterpret_cast<float4*>(hs + r * H + wv * kCols + 16 * t + 4 * q) =
-          make_float4(adj * x[t][0], adj * x[t][1], adj * x[t][2], adj * x[t][3]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hs[(4 * q + i) * H + wv * kCols + 16 * t + L] = adj[i] * x[t][i];
   }
 
-  // e -> A-operand layout by a wave-local 16x16 transpose through LDS (sT:
-  // this wave's TPW tiles); LDS is in order within a wave, no barrier.
-  __device__ __forceinline__ void stage(float* sT, int q, int r) {
-    if (G2K_ABL & 16) {
+  // softmax numerators of an arbitrary h (tf.nn.softmax max shift), in two
+  // halves around a barrier the caller provides: the row max exchange, then
+  // e and its row partials (published into red).
+  __device__ __forceinline__ void init_max(float* mred, int wv, int q, int L) const {
+    float m[4];
 #pragma unroll
-      for (int t = 0; t < TPW; ++t)
+    for (int i = 0; i < 4; ++i) {
+      m[i] = x[0][i];
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) av[t][ks] = e[t][ks];
-      return;
+      for (int t = 1; t < TPW; ++t) m[i] = fmaxf(m[i], x[t][i]);
     }
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-      *reinterpret_cast<float4*>(sT + t * kTTile + r * kTP + 4 * q) =
-          make_float4(e[t][0], e[t][1], e[t][2], e[t][3]);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) av[t][ks] = sT[t * kTTile + (4 * q + ks) * kTP + r];
+    const float r = reduce4_rows16<true>(m[0], m[1], m[2], m[3], L);
+    if (L < 4) mred[wv * 16 + 4 * q + reduce4_row(L)] = r;
   }
-
-  // softmax numerators of an arbitrary h (tf.nn.softmax max shift); publishes
-  // the row partial sums into `red` (64 floats) and stages e; barrier passed
-  // on return.  `mred`: 64 floats of scratch for the row max.
-  __device__ __forceinline__ void init(float* red, float* mred, float* sT, int wv, int q, int r) {
-    float m = x[0][0];
+  __device__ __forceinline__ void init_exp(float* red, const float* mred, int wv, int q, int L) {
+    float4 m = *reinterpret_cast<const float4*>(mred + 4 * q);
 #pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) m = fmaxf(m, x[t][i]);
-    m = max_rows4(m);
-    if (q == 0) mred[wv * 16 + r] = m;
-    __syncthreads();
-    m = mred[r];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) m = fmaxf(m, mred[16 * w + r]);
-    float p = 0.f;
+    for (int w = 1; w < NW; ++w) {
+      const float4 v = *reinterpret_cast<const float4*>(mred + 16 * w + 4 * q);
+      m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
+    }
+    const float mm[4] = {m.x, m.y, m.z, m.w};
+    float p[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        e[t][i] = __expf(x[t][i] - m);
-        p += e[t][i];
+        e[t][i] = __expf(x[t][i] - mm[i]);
+        p[i] += e[t][i];
       }
-    p = sum_rows4(p);
-    if (q == 0) red[wv * 16 + r] = p;
-    stage(sT, q, r);
+    publish(red, p, wv, q, L);
+  }
+
+  __device__ __forceinline__ void publish(float* red, float (&p)[4], int wv, int q, int L) const {
+    const float r = reduce4_rows16<false>(p[0], p[1], p[2], p[3], L);
+    if (L < 4) red[wv * 16 + 4 * q + reduce4_row(L)] = r;
+  }
+
+  // One frame with a workgroup barrier (g2k_recur_kernel).  b = As[L][4q..4q+3]
+  // of this frame; red_cur: the row partials of e (previous exchange);
+  // red_nxt: where this frame publishes its own.
+  __device__ __forceinline__ void step(const float4 b, const float* red_cur, float* red_nxt,
+                                       int wv, int q, int L) {
+    float4 z = *reinterpret_cast<const float4*>(red_cur + 4 * q);
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      const float4 v = *reinterpret_cast<const float4*>(red_cur + w * 16 + 4 * q);
+      z.x += v.x; z.y += v.y; z.z += v.z; z.w += v.w;
+    }
+    body(b, z, red_nxt, wv, q, L);
     __syncthreads();
   }
 
-  // One frame.  b = As[r][4q..4q+3] of this frame; red_cur: the row partials
-  // of e (previous exchange); red_nxt: where this frame publishes its own.
-  __device__ __forceinline__ void step(const float4 b, const float* red_cur, float* red_nxt,
-                                       float* sT, int wv, int q, int r) {
-    RSTAMP(0);
-    // B operand: As[r][k] / Z_k, k = 4q + ks
-    float4 z = make_float4(1.f, 1.f, 1.f, 1.f);
-    if (!(G2K_ABL & 4)) {
-      z = *reinterpret_cast<const float4*>(red_cur + 4 * q);
-#pragma unroll
-      for (int w = 1; w < NW; ++w) {
-        const float4 v = *reinterpret_cast<const float4*>(red_cur + w * 16 + 4 * q);
-        z.x += v.x; z.y += v.y; z.z += v.z; z.w += v.w;
-      }
-    }
-    const float b0 = b.x * rcp(z.x);
-    const float b1 = b.y * rcp(z.y);
-    const float b2 = b.z * rcp(z.z);
-    const float b3 = b.w * rcp(z.w);
-    RSTAMP(1);
+  // One frame without a workgroup barrier (fused scene kernel): z was polled
+  // from the previous exchange (seq words, see poll_frame); after publishing
+  // its row partials into red_nxt this wave raises its sequence word.
+  __device__ __forceinline__ void step_seq(const float4 b, const float4 z, float* red_nxt,
+                                           int* seq, int seq_val, int wv, int q, int L) {
+    body(b, z, red_nxt, wv, q, L);
+    asm volatile("" ::: "memory");   // partials land before the sequence word (LDS is in order)
+    if ((threadIdx.x & 63) == 0) *reinterpret_cast<volatile int*>(seq + wv) = seq_val;
+  }
+
+  __device__ __forceinline__ void body(const float4 b, const float4 z, float* red_nxt, int wv,
+                                       int q, int L) {
+    const float a0 = b.x * rcp(z.x);
+    const float a1 = b.y * rcp(z.y);
+    const float a2 = b.z * rcp(z.z);
+    const float a3 = b.w * rcp(z.w);
+    __builtin_amdgcn_sched_barrier(0);   // MFMAs back to back, k-step major
     f32x4 acc[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (G2K_ABL & 8) {
 #pragma unroll
-      for (int t = 0; t < TPW; ++t)
-        acc[t] = f32x4{av[t][0] * b0, av[t][1] * b1, av[t][2] * b2, av[t][3] * b3};
-    } else {
+    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, e[t][0], acc[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][0], b0, acc[t], 0, 0, 0);
+    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, e[t][1], acc[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][1], b1, acc[t], 0, 0, 0);
+    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, e[t][2], acc[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][2], b2, acc[t], 0, 0, 0);
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][3], b3, acc[t], 0, 0, 0);
-    }
-    RSTAMP(2);
-    float p = 0.f;
+    for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a3, e[t][3], acc[t], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    float p[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float v = acc[t][i];
-        const float ex = (G2K_ABL & 32) ? v : __expf(v);   // h' in [0, 1]: no max shift needed
         x[t][i] = v;
-        e[t][i] = ex;
-        p += ex;
+        e[t][i] = __expf(v);    // h' in [0, 1]: no max shift needed
+        p[i] += e[t][i];
       }
-    RSTAMP(3);
-    p = sum_rows4(p);
-    RSTAMP(4);
-    if (q == 0) red_nxt[wv * 16 + r] = p;
-    RSTAMP(5);
-    stage(sT, q, r);     // next frame's A operand, overlapping the barrier wait
-    RSTAMP(6);
-    if (!(G2K_ABL & 2)) __syncthreads();
-    RSTAMP(7);
-#ifdef G2K_STAMPS_RECUR
-    if (blockIdx.x == 0 && threadIdx.x == 0) g2k_rframe++;
-#endif
+    publish(red_nxt, p, wv, q, L);
   }
 };
 
@@ -819,7 +881,6 @@ __global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(RecurArgs a) {
   constexpr int kRB = 16 * NW;               // floats per row-partial buffer
   __shared__ __attribute__((aligned(16))) float sAs[kRecurChunk * kD * kD];
   __shared__ __attribute__((aligned(16))) float sRed[4 * kRB];
-  __shared__ __attribute__((aligned(16))) float sT[NW * TPW * kTTile];
   const int s = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6, q = lane >> 4, j = lane & 15;
   const int F = a.F, H = a.H;
@@ -840,11 +901,12 @@ __global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(RecurArgs a) {
     }
     a.metrics[(size_t)s * 8 + tid] = v;
   }
-  float* sTw = sT + wv * TPW * kTTile;
   // sRed: three row-partial buffers rotated per frame + one for the row max
   const float* last = nullptr;
   if (nf > 0) {
-    rec.init(sRed, sRed + 3 * kRB, sTw, wv, q, j);
+    rec.init_max(sRed + 3 * kRB, wv, q, j);
+    __syncthreads();
+    rec.init_exp(sRed, sRed + 3 * kRB, wv, q, j);   // published by the chunk barrier below
     int cur = 0;
     for (int fb = 0; fb < nf; fb += kRecurChunk) {
       const int cnt = (nf - fb) < kRecurChunk ? (nf - fb) : kRecurChunk;
@@ -863,7 +925,7 @@ __global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(RecurArgs a) {
       for (int fl = 0; fl < cnt; ++fl) {
         const float4 b = *reinterpret_cast<const float4*>(sAs + fl * kD * kD + j * kD + 4 * q);
         const int nxt = cur == 2 ? 0 : cur + 1;
-        rec.step(b, sRed + cur * kRB, sRed + nxt * kRB, sTw, wv, q, j);
+        rec.step(b, sRed + cur * kRB, sRed + nxt * kRB, wv, q, j);
         cur = nxt;
       }
       last = sRed + cur * kRB;
@@ -872,6 +934,457 @@ __global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(RecurArgs a) {
   }
   STAMP(12);
   rec.store(a.h_out + (size_t)s * kD * H, H, wv, q, j, last);
+}
+
+// ---------------------------------------------------------------------------
+// Fused step (the default): g2k_scene_kernel, one workgroup per scene,
+// wave-specialised.  Waves 0..3 (one per SIMD) run the frame-sequential
+// recurrence (Recur::step_seq); waves 4..4+NP-1 are producers that run the
+// frame-parallel body (frame_head + pred_tile below, frames pw, pw+NP, ...)
+// and hand each frame's As tile to the recurrence through an LDS ring with a
+// per-slot flag.  The two roles never share a barrier inside a chunk of
+// frames, so the recurrence's latency chain runs while the producers stream
+// predictions, targets and errors — and As never leaves the CU.
+// Frames are processed in chunks of lay.fc (<= 32, LDS permitting); the
+// workgroup barriers only at chunk boundaries.
+// ---------------------------------------------------------------------------
+constexpr int kSceneChunk = 32;
+constexpr int kRecW = 4;
+
+struct SceneLayout {
+  int fc, wcmax, np;
+  int o_wi, o_wo, o_nrm, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_red, o_pos;
+  int total;   // floats
+};
+
+__host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int fc, int NP) {
+  SceneLayout s;
+  s.fc = fc;
+  s.wcmax = (fc - 1) * stride + kT;
+  s.np = Nmax + 1;
+  int o = 0;
+  s.o_wi = o;    o += rup4(Nmax * kD);
+  s.o_wo = o;    o += rup4(kT * Nmax);
+  s.o_nrm = o;   o += rup4((s.wcmax + 2) * s.np);
+  s.o_v = o;     o += rup4((s.wcmax + 2) * kD);
+  s.o_small = o; o += 1024;
+  s.o_y = o;     o += NP * kD * kL2;
+  s.o_met = o;   o += NP * 8;
+  s.o_ring = o;  o += fc * kD * kD;
+  s.o_mring = o; o += fc * kL2 * kT;         // M = Wc @ cost per frame [24][8]
+  s.o_flag = o;  o += rup4(fc);
+  s.o_red = o;   o += 4 * 16 * kRecW;
+  s.o_pos = o;   o += rup4(s.wcmax * Nmax * 2);   // raw position window (LDS-DMA)
+  s.total = o;
+  return s;
+}
+
+// frame head: the g2k_lstm_mcr forward of one frame up to M^T (see the
+// comment above g2k_frames_kernel for the operand orientation); As goes to
+// `as_dst` (16 x 16), A / cost optionally to global.
+struct FrameHeadOut {
+  f32x4 mT0, mT1;
+};
+
+__device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float* vw,
+                                                   const float* sVe, float* as_dst, float* A_g,
+                                                   float* cost_g, int L, int q) {
+  const float ve0 = sVe[L], ve1 = sVe[kD + L];      // Ve[:, d = L]
+  const bool kq = q < 2;                           // k = 4q + ks < 8
+  f32x4 x0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+    x0 = mfma4(sm[SM_WII + L * kT + 4 * ks + q], vw[(4 * ks + q) * kD + L], x0);
+  float wv16[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) wv16[ks] = L < kT ? sm[SM_WV + L * (kD + 2) + 4 * q + ks] : 0.f;
+  f32x4 eN = {0.f, 0.f, 0.f, 0.f}, eT = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    eN = mfma4(wv16[ks], x0[ks], eN);      // E[4q+i][L]
+    eT = mfma4(x0[ks], wv16[ks], eT);      // E[L][4q+i]
+  }
+  const float bvL = sm[SM_BV + L];
+  float em[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = 4 * q + i;
+    if (kq) {
+      eN[i] = (eN[i] + fmaf(sm[SM_WV + t * (kD + 2) + kD], ve0,
+                            sm[SM_WV + t * (kD + 2) + kD + 1] * ve1)) + bvL;
+      const float rm = fmaf(sm[SM_WR + 2 * t], ve0 * ve0, sm[SM_WR + 2 * t + 1] * (ve1 * ve1));
+      em[i] = eN[i] * rm;
+    } else {
+      em[i] = 0.f;
+    }
+  }
+  if (L < kT) {
+    const float w16 = sm[SM_WV + L * (kD + 2) + kD], w17 = sm[SM_WV + L * (kD + 2) + kD + 1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d = 4 * q + i;
+      eT[i] = (eT[i] + fmaf(w16, sVe[d], w17 * sVe[kD + d])) + sm[SM_BV + d];
+    }
+  }
+  f32x4 aA = {0.f, 0.f, 0.f, 0.f}, cC = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const float gA = kq ? sm[SM_G + L * kT + 4 * q + ks] : 0.f;
+    const float gB = L < kT ? sm[SM_G + (4 * q + ks) * kT + L] : 0.f;
+    aA = mfma4(gA, em[ks], aA);      // A[4q+i][L]
+    cC = mfma4(eT[ks], gB, cC);      // cost[4q+i][L]
+  }
+  if (A_g) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) A_g[(4 * q + i) * kD + L] = aA[i];
+  }
+  if (cost_g && kq && L < kT) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cost_g[(4 * q + i) * kT + L] = cC[i];
+  }
+  // As = softmax(exp(A) / cumsum(exp(A), axis 0), axis -1)  (train.py:240)
+  {
+    float m_i[4], s_i[4];
+    float m = -INFINITY, sacc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lse_combine(m, sacc, aA[i], 1.0f);
+      m_i[i] = m; s_i[i] = sacc;
+    }
+    float mp = -INFINITY, sp = 0.f;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      const float mg = __shfl(m, L + 16 * g, 64);
+      const float sg = __shfl(sacc, L + 16 * g, 64);
+      if (g < q) lse_combine(mp, sp, mg, sg);
+    }
+    float ex[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float mr = m_i[i], sr = s_i[i];
+      if (q > 0) lse_combine(mr, sr, mp, sp);
+      const float R = __expf(aA[i] - mr) * rcp(sr);
+      ex[i] = __expf(R);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) as_dst[(4 * q + i) * kD + L] = ex[i] * rcp(row16_sum(ex[i]));
+  }
+  FrameHeadOut o;
+  o.mT0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  o.mT1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bool ok = kq && L < kL;
+    const float wc0 = ok ? sm[SM_WC + L * kT + 4 * q + ks] : 0.f;
+    const float wc1 = ok ? sm[SM_WC + (kL + L) * kT + 4 * q + ks] : 0.f;
+    o.mT0 = mfma4(cC[ks], wc0, o.mT0);   // M[L][4q+i]       (x rows)
+    o.mT1 = mfma4(cC[ks], wc1, o.mT1);   // M[12+L][4q+i]    (y rows)
+  }
+  return o;
+}
+
+// One 16-pedestrian tile of one frame: Y^T = Wo^T @ M^T (M = this frame's
+// [24][8] from the M ring), pred stores, a9 error terms (4 lanes per
+// pedestrian) accumulated into acc.  The contraction over t (8) uses
+// k = 4 ks + q, so two k-steps cover it without zero padding.
+__device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys,
+                                          float* pr, const float2 (&tg)[3], const uint8_t* pm,
+                                          int Nmax, int nact, int t, int L, int q, int lane,
+                                          float acc[5]) {
+  const int pp = lane >> 2, u = lane & 3;
+  const int n0 = 16 * t;
+  const int ne = n0 + pp;
+  const bool has_t = ne < nact && (pm ? pm[ne] != 0 : true);
+  f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int n = n0 + L, k = 4 * ks + q;
+    const float wo = n < nact ? sWo[k * Nmax + n] : 0.f;
+    const float bx = L < kL ? M[L * kT + k] : 0.f;
+    const float by = L < kL ? M[(kL + L) * kT + k] : 0.f;
+    y0 = mfma4(wo, bx, y0);   // Y[L][n0 + 4q + i]
+    y1 = mfma4(wo, by, y1);   // Y[12 + L][n0 + 4q + i]
+  }
+  if (L < kL) {
+    const int nb = n0 + 4 * q;
+    if (nb + 3 < Nmax && ((Nmax & 3) == 0)) {
+      *reinterpret_cast<float4*>(pr + L * Nmax + nb) = make_float4(y0[0], y0[1], y0[2], y0[3]);
+      *reinterpret_cast<float4*>(pr + (kL + L) * Nmax + nb) = make_float4(y1[0], y1[1], y1[2], y1[3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (nb + i < Nmax) { pr[L * Nmax + nb + i] = y0[i]; pr[(kL + L) * Nmax + nb + i] = y1[i]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float2*>(ys + (4 * q + i) * kL2 + 2 * L) = make_float2(y0[i], y1[i]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f, fx = 0.f, fy = 0.f;
+  const float2* yp = reinterpret_cast<const float2*>(ys + pp * kL2) + 3 * u;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float2 yv = yp[k];
+    const float dx = yv.x - tg[k].x, dy = yv.y - tg[k].y;
+    ea = fmaf(dx, dx, ea);
+    eb = fmaf(dx, dy, eb);
+    ec = fmaf(dy, dy, ec);
+    el2 += __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
+    fx = dx; fy = dy;
+  }
+  __builtin_amdgcn_wave_barrier();
+  ea += dpp<0xB1>(ea); ea += dpp<0x4E>(ea);
+  eb += dpp<0xB1>(eb); eb += dpp<0x4E>(eb);
+  ec += dpp<0xB1>(ec); ec += dpp<0x4E>(ec);
+  el2 += dpp<0xB1>(el2); el2 += dpp<0x4E>(el2);
+  fx = dpp<0xFF>(fx);   // quad_perm [3,3,3,3]: the fde vector lives in quarter 3
+  fy = dpp<0xFF>(fy);
+  if (has_t && u == 0) {
+    const float hm = 0.5f * (ea - ec);
+    const float lam = 0.5f * (ea + ec) + __builtin_amdgcn_sqrtf(fmaf(hm, hm, eb * eb));
+    const float fsq = fmaf(fx, fx, fy * fy);
+    acc[0] += __builtin_amdgcn_sqrtf(fmaxf(lam, 0.f)) * (1.0f / 12.0f);
+    acc[1] += 1.0f;
+    acc[2] += fsq;
+    acc[3] += el2 * (1.0f / 12.0f);
+    acc[4] += __builtin_amdgcn_sqrtf(fsq);
+  }
+}
+
+// Per-workgroup context of the scene kernel (LDS carve-up, scene scalars).
+struct SceneCtx {
+  float *sWi, *sWo, *sNrm, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sY, *sPos;
+  int* sFlag;
+  int s, tid, lane, wv, L, q, nact, nf, ntiles;
+};
+
+// LDS-DMA of a chunk's position window rows (train.py:76-79 window).
+template <int NT>
+__device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneCtx& c, int fb, int cnt) {
+  const int Nmax = a.d.Nmax, stride = a.d.stride;
+  const int wcc = (cnt - 1) * stride + kT;
+  dma4_copy_t<NT>(a.pos + ((size_t)c.s * a.d.W + fb * stride) * Nmax * 2, c.sPos, wcc * Nmax * 2,
+                  c.wv, c.lane);
+}
+
+// Chunk staging shared by both roles (every thread takes part).  The chunk's
+// position window is already in flight by LDS-DMA (scene_pos_dma).  Wait,
+// barrier; window norms ||(x, y)||_2 (train.py:79) into sNrm, barrier; V =
+// norms @ Wi for the chunk's window rows (train.py:179) and the two vislet
+// rows (Ve), barrier.  `mid1` runs before the second barrier, `mid2` before
+// the third.
+template <int NT, typename Mid1, typename Mid2>
+__device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout& lay,
+                                            const SceneCtx& c, int fb, int cnt, Mid1 mid1,
+                                            Mid2 mid2) {
+  const int Nmax = a.d.Nmax, stride = a.d.stride, np = lay.np;
+  const int wcc = (cnt - 1) * stride + kT;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  SSTAMP(102, c.tid == 0 && fb == 0);
+  __syncthreads();                                              // B1: window + weights landed
+  SSTAMP(1, c.tid == 0 && fb == 0);
+  for (int i = c.tid; i < wcc * Nmax; i += NT) {
+    const int w = i / Nmax, n = i - w * Nmax;
+    const float2 p = reinterpret_cast<const float2*>(c.sPos)[i];
+    c.sNrm[w * np + n] = n < c.nact ? sqrtf(fmaf(p.x, p.x, p.y * p.y)) : 0.f;
+  }
+  if (fb == 0 && c.tid < kD * kT) c.sm[SM_G + c.tid] *= a.lambda;   // ngh = lambda * ngh
+  mid1();
+  __syncthreads();                                              // B1b: norms
+  SSTAMP(101, c.tid == 0 && fb == 0);
+  for (int task = c.tid; task < (wcc + 2) * kD; task += NT) {
+    const int w0 = task >> 4, dcol = task & 15;
+    const int w = w0 < wcc ? w0 : lay.wcmax + (w0 - wcc);
+    const float* nr = c.sNrm + w * np;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+    int n = 0;
+    for (; n + 4 <= c.nact; n += 4) {
+      acc0 = fmaf(nr[n], c.sWi[n * kD + dcol], acc0);
+      acc1 = fmaf(nr[n + 1], c.sWi[(n + 1) * kD + dcol], acc1);
+      acc2 = fmaf(nr[n + 2], c.sWi[(n + 2) * kD + dcol], acc2);
+      acc3 = fmaf(nr[n + 3], c.sWi[(n + 3) * kD + dcol], acc3);
+    }
+    for (; n < c.nact; ++n) acc0 = fmaf(nr[n], c.sWi[n * kD + dcol], acc0);
+    c.sV[w * kD + dcol] = (acc0 + acc1) + (acc2 + acc3);
+  }
+  mid2();
+  __syncthreads();                                              // B2: V, Ve
+  SSTAMP(2, c.tid == 0 && fb == 0);
+}
+
+// Role 1: the recurrence (waves 0..3).
+template <int TPW, int NP>
+__device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneLayout& lay,
+                                                 const SceneCtx& c) {
+  constexpr int NT = 64 * (kRecW + NP);
+  constexpr int kRB = 16 * kRecW;
+  const int H = a.d.H;
+  Recur<TPW, kRecW> rc;
+  rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
+  int* seq = reinterpret_cast<int*>(c.sRed + 2 * kRB);   // 2 partial buffers, seq words, row max
+  for (int fb = 0; fb < c.nf; fb += lay.fc) {
+    const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
+    if (fb > 0) scene_pos_dma<NT>(a, c, fb, cnt);
+    scene_stage<NT>(
+        a, lay, c, fb, cnt,
+        [&] { if (fb == 0) rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L); },
+        [&] {
+          if (fb == 0) {
+            rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
+            asm volatile("" ::: "memory");
+            if (c.lane == 0) seq[c.wv] = 1;
+          }
+        });
+    __builtin_amdgcn_s_setprio(2);
+    for (int fl = 0; fl < cnt; ++fl) {
+      const int g = fb + fl;                 // global frame index
+      float4 b, z;
+      poll_frame(seq, g + 1, c.sFlag + fl, g + 1, c.sRing + fl * kD * kD + c.L * kD + 4 * c.q,
+                 c.sRed + (g & 1) * kRB + 4 * c.q, b, z);
+      rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 2, c.wv, c.q, c.L);
+      SSTAMP(40 + ((fb + fl) & 31), c.tid == 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    SSTAMP(80 + (c.wv & 15), c.lane == 0);
+    __syncthreads();                                            // B3: chunk done
+  }
+  __syncthreads();                                              // B4: metric partials
+  if (c.tid < 8) {
+    float v = 0.f;
+    if (c.tid < 5) {
+      if (c.nf > 0)
+        for (int p = 0; p < NP; ++p) v += c.sMet[p * 8 + c.tid];
+    } else if (c.tid == 5) {
+      v = (float)c.nf;
+    }
+    a.metrics[(size_t)c.s * 8 + c.tid] = v;
+  }
+  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L, c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);
+}
+
+// Role 2: the producers (waves 4..4+NP-1).
+template <int NP>
+__device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLayout& lay,
+                                               const SceneCtx& c) {
+  constexpr int NT = 64 * (kRecW + NP);
+  const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
+  const int pw = c.wv - kRecW, L = c.L, q = c.q, lane = c.lane, s = c.s, ntiles = c.ntiles;
+  float* ys = c.sY + pw * kD * kL2;
+  const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
+  // tile items of a chunk: item j -> frame j / ntiles, tile j % ntiles;
+  // this producer takes items pw, pw + NP, ...  (k-th item: j = pw + k * NP)
+  const int pp = lane >> 2, u = lane & 3;
+  float2 tgA[3] = {}, tgB[3] = {};
+  auto load_item = [&](int fb, int cnt, int k, float2 (&tg)[3]) {
+    const int j = pw + k * NP;
+    if (j >= cnt * ntiles) return;
+    const int fl = j / ntiles, t = j - fl * ntiles;
+    const int ne = 16 * t + pp;
+    const int nc = ne < Nmax ? ne : 0;
+    const float2* tp = reinterpret_cast<const float2*>(
+        a.targets + (((size_t)s * F + fb + fl) * Nmax + nc) * kL2) + 3 * u;
+    tg[0] = tp[0]; tg[1] = tp[1]; tg[2] = tp[2];
+  };
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int fb = 0; fb < c.nf; fb += lay.fc) {
+    const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
+    if (fb > 0) scene_pos_dma<NT>(a, c, fb, cnt);
+    scene_stage<NT>(a, lay, c, fb, cnt, [] {}, [] {});
+    load_item(fb, cnt, 0, tgA);       // first tiles' targets: in flight during the heads
+    load_item(fb, cnt, 1, tgB);
+    // phase 1 — the critical path: frame heads in frame order, As + M into
+    // the rings, then the frame's flag
+    for (int fl = pw; fl < cnt; fl += NP) {
+      const int f = fb + fl;
+      const FrameHeadOut hd =
+          frame_head(c.sm, c.sV + fl * stride * kD, c.sV + lay.wcmax * kD, c.sRing + fl * kD * kD,
+                     a.A_out ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
+                     a.cost_out ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr, L, q);
+      if (L < kL && q < 2) {
+        float* m = c.sMring + fl * kL2 * kT;
+        *reinterpret_cast<float4*>(m + L * kT + 4 * q) = make_float4(hd.mT0[0], hd.mT0[1], hd.mT0[2], hd.mT0[3]);
+        *reinterpret_cast<float4*>(m + (kL + L) * kT + 4 * q) = make_float4(hd.mT1[0], hd.mT1[1], hd.mT1[2], hd.mT1[3]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) *reinterpret_cast<volatile int*>(c.sFlag + fl) = f + 1;
+      SSTAMP(3 + (f & 31), lane == 0);
+    }
+    // phase 2 — predictions and errors, tiles spread over all producers
+#ifdef G2K_DIAG_SKIP_TILES
+    const int nitems = 0;   // diagnostic build only: no predictions / errors
+#else
+    const int nitems = cnt * ntiles > pw ? (cnt * ntiles - pw + NP - 1) / NP : 0;
+#endif
+    auto item = [&](int k, const float2 (&tg)[3]) {
+      const int j = pw + k * NP;
+      const int fl = j / ntiles, t = j - fl * ntiles;
+      const int f = fb + fl;
+      poll_flag(c.sFlag + fl, f + 1);          // M of this frame (maybe another producer's)
+      pred_tile(c.sMring + fl * kL2 * kT, c.sWo, ys, a.pred + ((size_t)s * F + f) * kL2 * Nmax, tg, pm, Nmax, c.nact, t,
+                L, q, lane, acc);
+    };
+    for (int k = 0; k < nitems; k += 2) {
+      item(k, tgA);
+      load_item(fb, cnt, k + 2, tgA);
+      if (k + 1 < nitems) {
+        item(k + 1, tgB);
+        load_item(fb, cnt, k + 3, tgB);
+      }
+    }
+    SSTAMP(80 + (c.wv & 15), lane == 0);
+    __syncthreads();                                            // B3: chunk done
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const float v = wave_sum(acc[k]);
+    if (lane == 0) c.sMet[pw * 8 + k] = v;
+  }
+  __syncthreads();                                              // B4
+}
+
+template <int TPW, int NP>
+__global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a, SceneLayout lay) {
+  constexpr int NT = 64 * (kRecW + NP);
+  constexpr int kRB = 16 * kRecW;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  SceneCtx c;
+  c.s = blockIdx.x;
+  c.tid = threadIdx.x; c.lane = c.tid & 63; c.wv = c.tid >> 6; c.L = c.lane & 15; c.q = c.lane >> 4;
+  const int Nmax = a.d.Nmax, F = a.d.F;
+  c.nact = clampi(a.n_active[c.s], 0, Nmax);
+  c.nf = a.n_frames ? clampi(a.n_frames[c.s], 0, F) : F;
+  c.ntiles = (Nmax + 15) >> 4;
+  c.sWi = smem + lay.o_wi; c.sWo = smem + lay.o_wo; c.sNrm = smem + lay.o_nrm; c.sV = smem + lay.o_v;
+  c.sm = smem + lay.o_small; c.sMet = smem + lay.o_met; c.sRing = smem + lay.o_ring;
+  c.sMring = smem + lay.o_mring; c.sRed = smem + lay.o_red; c.sPos = smem + lay.o_pos;
+  c.sY = smem + lay.o_y;
+  c.sFlag = reinterpret_cast<int*>(smem + lay.o_flag);
+  SSTAMP(0, c.tid == 0);
+  // frames beyond n_frames: zero predictions
+  for (int i = c.tid; i < (F - c.nf) * kL2 * Nmax; i += NT)
+    a.pred[((size_t)c.s * F + c.nf) * kL2 * Nmax + i] = 0.f;
+  if (c.nf > 0) {
+    const int wv = c.wv, lane = c.lane, np = lay.np;
+    scene_pos_dma<NT>(a, c, 0, c.nf < lay.fc ? c.nf : lay.fc);   // critical path first
+    dma4_copy_t<NT>(a.w.Wi, c.sWi, Nmax * kD, wv, lane);
+    dma4_copy_t<NT>(a.w.Wo, c.sWo, kT * Nmax, wv, lane);
+    dma4_copy_t<NT>(a.w.Wii, c.sm + SM_WII, kD * kT, wv, lane);
+    dma4_copy_t<NT>(a.G + (size_t)c.s * kD * kT, c.sm + SM_G, kD * kT, wv, lane);
+    dma4_copy_t<NT>(a.w.Wv, c.sm + SM_WV, kT * (kD + 2), wv, lane);
+    dma4_copy_t<NT>(a.w.bv, c.sm + SM_BV, kD, wv, lane);
+    dma4_copy_t<NT>(a.w.Wr, c.sm + SM_WR, kT * 2, wv, lane);
+    dma4_copy_t<NT>(a.w.Wc, c.sm + SM_WC, kL2 * kT, wv, lane);
+    const float* vis = a.vislet + (size_t)c.s * 2 * Nmax;
+    dma4_copy_t<NT>(vis, c.sNrm + lay.wcmax * np, Nmax, wv, lane);
+    dma4_copy_t<NT>(vis + Nmax, c.sNrm + (lay.wcmax + 1) * np, Nmax, wv, lane);
+    if (c.tid < kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;   // sequence words
+    if (c.tid < lay.fc) c.sFlag[c.tid] = 0;              // flags hold (global frame + 1)
+  }
+  if (c.wv < kRecW)
+    scene_recurrence<TPW, NP>(a, lay, c);
+  else
+    scene_producer<NP>(a, lay, c);
+  SSTAMP(100, c.tid == 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1128,6 +1641,59 @@ int launch_recur(const RecurArgs& r, int S, hipStream_t st) {
   return G2K_OK;
 }
 
+// Fused scene kernel geometry: producer waves (NP) and the frames-per-chunk
+// that fits LDS.  NP = 8 by default (12 waves: one recurrence + two producer
+// waves per SIMD); G2K_SCENE_NP in {4, 8, 12} is a tuning override.
+int scene_producers(int H) {
+  int np = 8;
+  const char* env = getenv("G2K_SCENE_NP");
+  if (env && (atoi(env) == 4 || atoi(env) == 8 || atoi(env) == 12)) np = atoi(env);
+  if (H >= 512) np = 4;            // TPW 8 needs > 128 VGPRs: at most 512 threads
+  return np;
+}
+
+SceneLayout scene_layout(const g2k_dims* d, int NP) {
+  int fc = d->F < 1 ? 1 : (d->F < kSceneChunk ? d->F : kSceneChunk);
+  SceneLayout l = scene_layout_fc(d->Nmax, d->stride, fc, NP);
+  while ((int64_t)l.total * 4 > 160 * 1024 && fc > 1) {
+    fc = (fc + 1) / 2;
+    l = scene_layout_fc(d->Nmax, d->stride, fc, NP);
+  }
+  return l;
+}
+
+bool use_split_step() {
+  const char* env = getenv("G2K_STEP_SPLIT");   // A/B switch: the two-kernel step
+  return env && atoi(env) == 1;
+}
+
+template <int NP>
+int launch_scene_np(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
+  const size_t lds = (size_t)l.total * 4;
+  const dim3 g(a.d.S), b(64 * (kRecW + NP));
+  switch (a.d.H / 64) {
+    case 1: hipLaunchKernelGGL((g2k_scene_kernel<1, NP>), g, b, lds, st, a, l); break;
+    case 2: hipLaunchKernelGGL((g2k_scene_kernel<2, NP>), g, b, lds, st, a, l); break;
+    case 4: hipLaunchKernelGGL((g2k_scene_kernel<4, NP>), g, b, lds, st, a, l); break;
+    default: return set_err(G2K_EUNSUPPORTED, "H=%d unsupported with %d producer waves", a.d.H, NP);
+  }
+  return G2K_OK;
+}
+
+int launch_scene(const StepArgs& a, const SceneLayout& l, int NP, hipStream_t st) {
+  if (a.d.H == 512) {
+    hipLaunchKernelGGL((g2k_scene_kernel<8, 4>), dim3(a.d.S), dim3(64 * (kRecW + 4)),
+                       (size_t)l.total * 4, st, a, l);
+    return G2K_OK;
+  }
+  switch (NP) {
+    case 4: return launch_scene_np<4>(a, l, st);
+    case 8: return launch_scene_np<8>(a, l, st);
+    case 12: return launch_scene_np<12>(a, l, st);
+    default: return set_err(G2K_EUNSUPPORTED, "NP=%d", NP);
+  }
+}
+
 int validate_H(int H) {
   if (H < 64 || H > 512 || (H % 64) || (H / 64) == 3 || (H / 64) == 5 || (H / 64) == 6 ||
       (H / 64) == 7)
@@ -1148,14 +1714,9 @@ int g2k_abi_version(void) { return G2K_ABI_VERSION; }
 
 const char* g2k_last_error(void) { return g_err; }
 
-#ifdef G2K_STAMPS_RECUR
-int g2k_debug_rstamps(unsigned long long* host) {
-  int z = 0;
-  hipMemcpyToSymbol(HIP_SYMBOL(g2k_rframe), &z, sizeof(int));
-  return 0;
-}
-int g2k_debug_rstamps_get(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2k_rstamps), 16 * sizeof(unsigned long long));
+#ifdef G2K_STAMPS_SCENE
+int g2k_debug_sstamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2k_sstamps), 4 * 128 * sizeof(unsigned long long));
 }
 #endif
 #ifdef G2K_STAMPS
@@ -1209,6 +1770,15 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
   a.ws_as = static_cast<float*>(workspace);
   a.ws_part = a.ws_as + (size_t)d->S * d->F * kD * kD;
   hipStream_t st = (hipStream_t)stream;
+  if (!use_split_step()) {
+    const int NP = scene_producers(d->H);
+    const SceneLayout l = scene_layout(d, NP);
+    if ((int64_t)l.total * 4 > 160 * 1024)
+      return set_err(G2K_ELDS, "Nmax=%d, stride=%d needs %lld bytes of LDS", d->Nmax, d->stride,
+                     (long long)l.total * 4);
+    if ((rc = launch_scene(a, l, NP, st))) return rc;
+    return check_launch("g2k_step_fused_f32/scene");
+  }
   if (d->F > 0) {
     hipLaunchKernelGGL(g2k_frames_kernel, dim3(p.nchunk, d->S), dim3(kNT), p.lds_bytes, st, a);
     if ((rc = check_launch("g2k_step_fused_f32/frames"))) return rc;

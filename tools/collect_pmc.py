@@ -6,7 +6,7 @@ streaming reads on gfx950 -> x2; WRITE_SIZE exact for 16-B stores; values in KiB
 usage: collect_pmc.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON"""
 import collections, csv, glob, json, os, sys
 
-KERNELS = ("g2k_frames_kernel", "g2k_recur_kernel")
+KERNELS = ("g2k_scene_kernel", "g2k_frames_kernel", "g2k_recur_kernel")
 
 
 def per_kernel(d, counter):

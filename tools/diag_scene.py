@@ -1,0 +1,41 @@
+"""Diagnostic: timeline (s_memtime ticks) of scene-kernel workgroups 0, 85,
+170, 255 — staging barriers, per-frame producer flags, per-frame recurrence
+completion, producer chunk ends.  Builds a separate -DG2K_STAMPS_SCENE library
+into /tmp; never the shipped one."""
+import ctypes, os, subprocess, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from multimodaltraj_2_amd import _lib, build, frame_step as fs
+from multimodaltraj_2_amd.synthetic import make_batch, CONFIGS
+
+out = "/tmp/libg2k_sstamps.so"
+subprocess.run([build.HIPCC, *build.FLAGS, "-DG2K_STAMPS_SCENE", "-o", out, *build.SRC], check=True)
+lib = _lib.load(out)
+_lib._lib = lib
+lib.g2k_debug_sstamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+cfg = sys.argv[1] if len(sys.argv) > 1 else "eth_hotel_synth"
+c = CONFIGS[cfg]
+S = c["S"] if c["S"] <= 256 else c["S"] // 8
+b = make_batch(S, c["Nmax"], c["H"])
+dev = torch.device("cuda")
+p = fs.init_params(c["Nmax"], device=dev)
+t = b.to_device(dev)
+for _ in range(10):
+    o = fs.step_fused(p, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+torch.cuda.synchronize()
+st = (ctypes.c_ulonglong * 512)()
+lib.g2k_debug_sstamps(st)
+v = np.array(st[:], dtype=np.int64).reshape(4, 128)
+t0 = v[:, 0].min()
+F = b.F
+for k in range(4):
+    blk = 85 * k
+    if blk >= S:
+        continue
+    r = v[k] - t0
+    print(f"== WG {blk} n_active={b.n_active[blk]}: start {r[0]} vmcnt {r[102]} B1 {r[1]} B1b {r[101]} B2 {r[2]} end {r[100]}")
+    print("   producer flags:", " ".join(str(x) for x in r[3:3 + F]))
+    print("   recur done    :", " ".join(str(x) for x in r[40:40 + F]))
+    print("   recur per-frame:", " ".join(str(x) for x in np.diff(r[40:40 + F])))
+    print("   wave chunk end:", " ".join(str(x) for x in r[80:80 + 12]))
