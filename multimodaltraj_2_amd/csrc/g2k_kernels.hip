@@ -950,10 +950,19 @@ __global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(RecurArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kSceneChunk = 32;
 constexpr int kRecW = 4;
+// scene-kernel small block: the split path's offsets plus weight-derived
+// matrices (DESIGN.md "frame head"): K1 = [Wv16 @ Wii | Wv16.. | Wv17.. | 1 | 0]
+// ([8][12]), K2 = Wc @ K1 ([24][12]), bvg = bv @ g ([8]).
+constexpr int SM_K1 = 640;
+constexpr int SM_BVG = 736;
+constexpr int SM_K2 = 752;
+constexpr int kSceneSmall = 1088;
+constexpr int kKA = 12;        // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
 
 struct SceneLayout {
   int fc, wcmax, np;
-  int o_wi, o_wo, o_nrm, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_red, o_pos;
+  int o_wi, o_wo, o_nrm, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_red, o_pos, o_vg,
+      o_wig;
   int total;   // floats
 };
 
@@ -967,9 +976,11 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_wo = o;    o += rup4(kT * Nmax);
   s.o_nrm = o;   o += rup4((s.wcmax + 2) * s.np);
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);
-  s.o_small = o; o += 1024;
+  s.o_small = o; o += kSceneSmall;
   s.o_y = o;     o += NP * kD * kL2;
   s.o_met = o;   o += NP * 8;
+  s.o_vg = o;    o += rup4((s.wcmax + 2) * kT);    // VG = V @ g rows (window + vislet)
+  s.o_wig = o;   o += rup4(Nmax * kT);             // Wig = Wi @ g
   s.o_ring = o;  o += fc * kD * kD;
   s.o_mring = o; o += fc * kL2 * kT;         // M = Wc @ cost per frame [24][8]
   s.o_flag = o;  o += rup4(fc);
@@ -979,107 +990,151 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   return s;
 }
 
-// frame head: the g2k_lstm_mcr forward of one frame up to M^T (see the
-// comment above g2k_frames_kernel for the operand orientation); As goes to
-// `as_dst` (16 x 16), A / cost optionally to global.
 struct FrameHeadOut {
-  f32x4 mT0, mT1;
+  f32x4 mT0, mT1;   // M[L][4q+i] (x rows), M[12+L][4q+i] (y rows)
 };
 
-__device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float* vw,
-                                                   const float* sVe, float* as_dst, float* A_g,
-                                                   float* cost_g, int L, int q) {
-  const float ve0 = sVe[L], ve1 = sVe[kD + L];      // Ve[:, d = L]
-  const bool kq = q < 2;                           // k = 4q + ks < 8
-  f32x4 x0 = {0.f, 0.f, 0.f, 0.f};
+// Partner lane's value across lane groups (q ^ 1 by permlane16, q ^ 2 by
+// permlane32): of the pair a swap returns, one element is this lane's own
+// value, the other the partner's.
+__device__ __forceinline__ float partner16(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return a[0] == __float_as_uint(v) ? __uint_as_float(a[1]) : __uint_as_float(a[0]);
+}
+__device__ __forceinline__ float partner32(float v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return a[0] == __float_as_uint(v) ? __uint_as_float(a[1]) : __uint_as_float(a[0]);
+}
+
+// As = softmax(exp(A) / cumsum(exp(A), axis 0), axis -1)  (train.py:240) of
+// one frame's A in the MFMA result layout (column L, rows 4q + i), written
+// to as_dst [16][16].  The ratio exp(A_r) / sum_{k<=r} exp(A_k) is invariant
+// to a per-column shift: with the column max M, e = exp(A - M) lies in (0, 1]
+// and the prefix sums (in-lane, then across lane groups by permlane swaps)
+// cannot overflow.  If a prefix sum underflows (the column's leading rows are
+// ~87 below its max) the wave redoes the column with a running (max, sum)
+// pair, which is exact for any finite A.  Then a 16-lane row softmax of
+// values in (0, 1].
+__device__ __forceinline__ void attn_weights(const f32x4 aA, float* as_dst, int L, int q) {
+  float mx = fmaxf(fmaxf(aA[0], aA[1]), fmaxf(aA[2], aA[3]));
+  mx = fmaxf(mx, partner16(mx));
+  mx = fmaxf(mx, partner32(mx));
+  float e[4], p[4];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-    x0 = mfma4(sm[SM_WII + L * kT + 4 * ks + q], vw[(4 * ks + q) * kD + L], x0);
-  float wv16[4];
+  for (int i = 0; i < 4; ++i) e[i] = __expf(aA[i] - mx);
+  p[0] = e[0];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) wv16[ks] = L < kT ? sm[SM_WV + L * (kD + 2) + 4 * q + ks] : 0.f;
-  f32x4 eN = {0.f, 0.f, 0.f, 0.f}, eT = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    eN = mfma4(wv16[ks], x0[ks], eN);      // E[4q+i][L]
-    eT = mfma4(x0[ks], wv16[ks], eT);      // E[L][4q+i]
-  }
-  const float bvL = sm[SM_BV + L];
-  float em[4];
+  for (int i = 1; i < 4; ++i) p[i] = p[i - 1] + e[i];
+  const float t1 = partner16(p[3]), t2 = partner32(p[3]), t3 = partner32(t1);
+  const float pre = ((q & 2) ? t2 + t3 : 0.f) + ((q & 1) ? t1 : 0.f);   // groups before q
+  float R[4];
+  bool bad = false;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int t = 4 * q + i;
-    if (kq) {
-      eN[i] = (eN[i] + fmaf(sm[SM_WV + t * (kD + 2) + kD], ve0,
-                            sm[SM_WV + t * (kD + 2) + kD + 1] * ve1)) + bvL;
-      const float rm = fmaf(sm[SM_WR + 2 * t], ve0 * ve0, sm[SM_WR + 2 * t + 1] * (ve1 * ve1));
-      em[i] = eN[i] * rm;
-    } else {
-      em[i] = 0.f;
-    }
+    const float P = pre + p[i];
+    bad |= !(P >= 1e-30f);
+    R[i] = e[i] * rcp(P);
   }
-  if (L < kT) {
-    const float w16 = sm[SM_WV + L * (kD + 2) + kD], w17 = sm[SM_WV + L * (kD + 2) + kD + 1];
+  if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+    // running (max, sum exp) down the rows; exclusive prefix over the groups
+    float m_i[4], s_i[4];
+    float m = aA[0], sacc = 1.0f;
+    m_i[0] = m; s_i[0] = sacc;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      lse_combine(m, sacc, aA[i], 1.0f);
+      m_i[i] = m; s_i[i] = sacc;
+    }
+    const float m1 = partner16(m), s1 = partner16(sacc);
+    const float m2 = partner32(m), s2 = partner32(sacc);
+    const float m3 = partner32(m1), s3 = partner32(s1);
+    float pm = m2, ps = s2;
+    lse_combine(pm, ps, m3, s3);
+    float mp = -INFINITY, sp = 0.f;
+    if (q & 2) { mp = pm; sp = ps; }
+    if (q & 1) {
+      if (q & 2) lse_combine(mp, sp, m1, s1);
+      else { mp = m1; sp = s1; }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int d = 4 * q + i;
-      eT[i] = (eT[i] + fmaf(w16, sVe[d], w17 * sVe[kD + d])) + sm[SM_BV + d];
+      float mr = m_i[i], sr = s_i[i];
+      if (q > 0) lse_combine(mr, sr, mp, sp);
+      R[i] = __expf(aA[i] - mr) * rcp(sr);
     }
   }
-  f32x4 aA = {0.f, 0.f, 0.f, 0.f}, cC = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float ex = __expf(R[i]);
+    as_dst[(4 * q + i) * kD + L] = ex * rcp(row16_sum(ex));
+  }
+}
+
+// frame head: the g2k_lstm_mcr forward of one frame up to M (models/
+// g2k_lstm_mcr.py:99-124 with train.py:178-195), reassociated around the
+// weight-derived K1 / K2 (computed once per workgroup in scene_stage):
+//   E    = K1 @ Uaug      Uaug = [U (8 window rows of V); Ve0; Ve1; bv; 0]
+//        = Wv[:, :16] @ (Wii @ U) + Wv[:, 16:18] @ Ve + bv          (:105, 112)
+//   A    = g @ (E * Rm)                                             (:105-106)
+//   cost = E @ g = K1 @ VGaug        (VGaug = Uaug @ g, rows of VG)  (:112-113)
+//   M    = Wc @ cost = K2 @ VGaug                                   (:119)
+// Contractions over the 12 augmented rows use k = 4 ks + q (3 k-steps);
+// A contracts over t = 4q + ks (rows of E as the MFMA left them).
+// As goes to `as_dst`; the x / y row tiles of M^T are returned (M[L][4q+i]).
+__device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float* sV,
+                                                   const float* sVG, int wrow0, int wcmax,
+                                                   const float (&rm)[4], float* as_dst,
+                                                   float* A_g, float* cost_g, int L, int q) {
+  float ka[3], ua[3], va[3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const int k = 4 * ks + q;
+    ka[ks] = L < kT ? sm[SM_K1 + L * kKA + k] : 0.f;
+    if (ks < 2) {
+      ua[ks] = sV[(wrow0 + k) * kD + L];
+      va[ks] = L < kT ? sVG[(wrow0 + k) * kT + L] : 0.f;
+    } else {
+      ua[ks] = q < 2 ? sV[(wcmax + q) * kD + L] : (q == 2 ? sm[SM_BV + L] : 0.f);
+      va[ks] = L >= kT ? 0.f : (q < 2 ? sVG[(wcmax + q) * kT + L] : (q == 2 ? sm[SM_BVG + L] : 0.f));
+    }
+  }
+  f32x4 eN = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);          // E[4q+i][L]
+  FrameHeadOut o;
+  o.mT0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  o.mT1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const int k = 4 * ks + q;
+    const float bx = L < kL ? sm[SM_K2 + L * kKA + k] : 0.f;
+    const float by = L < kL ? sm[SM_K2 + (kL + L) * kKA + k] : 0.f;
+    o.mT0 = mfma4(va[ks], bx, o.mT0);   // M[L][4q+i]       (x rows)
+    o.mT1 = mfma4(va[ks], by, o.mT1);   // M[12+L][4q+i]    (y rows)
+  }
+  float em[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) em[i] = eN[i] * rm[i];                      // rm = 0 for t >= 8
+  f32x4 aA = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    const float gA = kq ? sm[SM_G + L * kT + 4 * q + ks] : 0.f;
-    const float gB = L < kT ? sm[SM_G + (4 * q + ks) * kT + L] : 0.f;
-    aA = mfma4(gA, em[ks], aA);      // A[4q+i][L]
-    cC = mfma4(eT[ks], gB, cC);      // cost[4q+i][L]
+    const float gA = q < 2 ? sm[SM_G + L * kT + 4 * q + ks] : 0.f;       // g[r = L][t]
+    aA = mfma4(gA, em[ks], aA);                                          // A[4q+i][L]
   }
   if (A_g) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) A_g[(4 * q + i) * kD + L] = aA[i];
   }
-  if (cost_g && kq && L < kT) {
+  if (cost_g) {
+    f32x4 cC = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cost_g[(4 * q + i) * kT + L] = cC[i];
-  }
-  // As = softmax(exp(A) / cumsum(exp(A), axis 0), axis -1)  (train.py:240)
-  {
-    float m_i[4], s_i[4];
-    float m = -INFINITY, sacc = 0.f;
+    for (int ks = 0; ks < 3; ++ks) cC = mfma4(ka[ks], va[ks], cC);      // cost[4q+i][L]
+    if (q < 2 && L < kT) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      lse_combine(m, sacc, aA[i], 1.0f);
-      m_i[i] = m; s_i[i] = sacc;
+      for (int i = 0; i < 4; ++i) cost_g[(4 * q + i) * kT + L] = cC[i];
     }
-    float mp = -INFINITY, sp = 0.f;
-#pragma unroll
-    for (int g = 0; g < 3; ++g) {
-      const float mg = __shfl(m, L + 16 * g, 64);
-      const float sg = __shfl(sacc, L + 16 * g, 64);
-      if (g < q) lse_combine(mp, sp, mg, sg);
-    }
-    float ex[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float mr = m_i[i], sr = s_i[i];
-      if (q > 0) lse_combine(mr, sr, mp, sp);
-      const float R = __expf(aA[i] - mr) * rcp(sr);
-      ex[i] = __expf(R);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) as_dst[(4 * q + i) * kD + L] = ex[i] * rcp(row16_sum(ex[i]));
   }
-  FrameHeadOut o;
-  o.mT0 = f32x4{0.f, 0.f, 0.f, 0.f};
-  o.mT1 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const bool ok = kq && L < kL;
-    const float wc0 = ok ? sm[SM_WC + L * kT + 4 * q + ks] : 0.f;
-    const float wc1 = ok ? sm[SM_WC + (kL + L) * kT + 4 * q + ks] : 0.f;
-    o.mT0 = mfma4(cC[ks], wc0, o.mT0);   // M[L][4q+i]       (x rows)
-    o.mT1 = mfma4(cC[ks], wc1, o.mT1);   // M[12+L][4q+i]    (y rows)
-  }
+  attn_weights(aA, as_dst, L, q);
   return o;
 }
 
@@ -1153,7 +1208,7 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
 
 // Per-workgroup context of the scene kernel (LDS carve-up, scene scalars).
 struct SceneCtx {
-  float *sWi, *sWo, *sNrm, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sY, *sPos;
+  float *sWi, *sWo, *sNrm, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sY, *sPos, *sVG, *sWig;
   int* sFlag;
   int s, tid, lane, wv, L, q, nact, nf, ntiles;
 };
@@ -1163,8 +1218,11 @@ template <int NT>
 __device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneCtx& c, int fb, int cnt) {
   const int Nmax = a.d.Nmax, stride = a.d.stride;
   const int wcc = (cnt - 1) * stride + kT;
-  dma4_copy_t<NT>(a.pos + ((size_t)c.s * a.d.W + fb * stride) * Nmax * 2, c.sPos, wcc * Nmax * 2,
-                  c.wv, c.lane);
+  const float* src = a.pos + ((size_t)c.s * a.d.W + fb * stride) * Nmax * 2;
+  if ((Nmax & 1) == 0 && (((uintptr_t)a.pos) & 15) == 0)
+    dma_copy_n<NT>(src, c.sPos, wcc * Nmax / 2, c.wv, c.lane);      // 16-B granules
+  else
+    dma4_copy_t<NT>(src, c.sPos, wcc * Nmax * 2, c.wv, c.lane);
 }
 
 // Chunk staging shared by both roles (every thread takes part).  The chunk's
@@ -1173,13 +1231,16 @@ __device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneCtx&
 // norms @ Wi for the chunk's window rows (train.py:179) and the two vislet
 // rows (Ve), barrier.  `mid1` runs before the second barrier, `mid2` before
 // the third.
-template <int NT, typename Mid1, typename Mid2>
+template <int NT, int VMC, typename Mid1, typename Mid2>
 __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int fb, int cnt, Mid1 mid1,
                                             Mid2 mid2) {
   const int Nmax = a.d.Nmax, stride = a.d.stride, np = lay.np;
   const int wcc = (cnt - 1) * stride + kT;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // VMC = vector-memory ops this wave issued after the LDS-DMA that may stay
+  // in flight (the recurrence's h loads at the first chunk)
+  if (VMC > 0 && fb == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   SSTAMP(102, c.tid == 0 && fb == 0);
   __syncthreads();                                              // B1: window + weights landed
   SSTAMP(1, c.tid == 0 && fb == 0);
@@ -1188,24 +1249,69 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
     const float2 p = reinterpret_cast<const float2*>(c.sPos)[i];
     c.sNrm[w * np + n] = n < c.nact ? sqrtf(fmaf(p.x, p.x, p.y * p.y)) : 0.f;
   }
-  if (fb == 0 && c.tid < kD * kT) c.sm[SM_G + c.tid] *= a.lambda;   // ngh = lambda * ngh
+  if (fb == 0) {
+    // weight-derived matrices of the frame head (see frame_head), once:
+    // K1 = [Wv16 @ Wii | Wv[:,16] | Wv[:,17] | 1 | 0], Wig = Wi @ g, bvg = bv @ g
+    const float* sm = c.sm;
+    const float lam = a.lambda;
+    const int nk1 = kT * kKA, nwig = Nmax * kT;
+    for (int task = c.tid; task < nk1 + nwig + kT; task += NT) {
+      if (task < nk1) {
+        const int t = task / kKA, k = task - t * kKA;
+        float v;
+        if (k < kT) {
+          v = 0.f;
+          for (int d = 0; d < kD; ++d) v = fmaf(sm[SM_WV + t * (kD + 2) + d], sm[SM_WII + d * kT + k], v);
+        } else {
+          v = k == 8 ? sm[SM_WV + t * (kD + 2) + kD] : k == 9 ? sm[SM_WV + t * (kD + 2) + kD + 1]
+                                                      : (k == 10 ? 1.f : 0.f);
+        }
+        c.sm[SM_K1 + task] = v;
+      } else if (task < nk1 + nwig) {
+        const int i = task - nk1, n = i / kT, t2 = i - n * kT;
+        float v = 0.f;
+        for (int d = 0; d < kD; ++d) v = fmaf(c.sWi[n * kD + d], sm[SM_G + d * kT + t2], v);
+        c.sWig[n * kT + t2] = lam * v;
+      } else {
+        const int t2 = task - nk1 - nwig;
+        float v = 0.f;
+        for (int d = 0; d < kD; ++d) v = fmaf(sm[SM_BV + d], sm[SM_G + d * kT + t2], v);
+        c.sm[SM_BVG + t2] = lam * v;
+      }
+    }
+  }
   mid1();
-  __syncthreads();                                              // B1b: norms
+  __syncthreads();                                              // B1b: norms, K1, K2, Wig
   SSTAMP(101, c.tid == 0 && fb == 0);
-  for (int task = c.tid; task < (wcc + 2) * kD; task += NT) {
-    const int w0 = task >> 4, dcol = task & 15;
+  if (fb == 0) {
+    if (c.tid < kD * kT) c.sm[SM_G + c.tid] *= a.lambda;       // ngh = lambda * ngh
+    for (int task = c.tid; task < kL2 * kKA; task += NT) {     // K2 = Wc @ K1
+      const int j = task / kKA, k = task - j * kKA;
+      float v = 0.f;
+      for (int t = 0; t < kT; ++t) v = fmaf(c.sm[SM_WC + j * kT + t], c.sm[SM_K1 + t * kKA + k], v);
+      c.sm[SM_K2 + task] = v;
+    }
+  }
+  // V = norms @ Wi (train.py:179) and VG = norms @ Wig for the chunk's window
+  // rows and the two vislet rows (Ve)
+  for (int task = c.tid; task < (wcc + 2) * (kD + kT); task += NT) {
+    const int w0 = task / (kD + kT), col = task - w0 * (kD + kT);
     const int w = w0 < wcc ? w0 : lay.wcmax + (w0 - wcc);
     const float* nr = c.sNrm + w * np;
+    const float* src = col < kD ? c.sWi + col : c.sWig + (col - kD);
+    const int ld = col < kD ? kD : kT;
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
     int n = 0;
     for (; n + 4 <= c.nact; n += 4) {
-      acc0 = fmaf(nr[n], c.sWi[n * kD + dcol], acc0);
-      acc1 = fmaf(nr[n + 1], c.sWi[(n + 1) * kD + dcol], acc1);
-      acc2 = fmaf(nr[n + 2], c.sWi[(n + 2) * kD + dcol], acc2);
-      acc3 = fmaf(nr[n + 3], c.sWi[(n + 3) * kD + dcol], acc3);
+      acc0 = fmaf(nr[n], src[n * ld], acc0);
+      acc1 = fmaf(nr[n + 1], src[(n + 1) * ld], acc1);
+      acc2 = fmaf(nr[n + 2], src[(n + 2) * ld], acc2);
+      acc3 = fmaf(nr[n + 3], src[(n + 3) * ld], acc3);
     }
-    for (; n < c.nact; ++n) acc0 = fmaf(nr[n], c.sWi[n * kD + dcol], acc0);
-    c.sV[w * kD + dcol] = (acc0 + acc1) + (acc2 + acc3);
+    for (; n < c.nact; ++n) acc0 = fmaf(nr[n], src[n * ld], acc0);
+    const float v = (acc0 + acc1) + (acc2 + acc3);
+    if (col < kD) c.sV[w * kD + col] = v;
+    else c.sVG[w * kT + col - kD] = v;
   }
   mid2();
   __syncthreads();                                              // B2: V, Ve
@@ -1220,12 +1326,14 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   constexpr int kRB = 16 * kRecW;
   const int H = a.d.H;
   Recur<TPW, kRecW> rc;
+  asm volatile("" ::: "memory");   // h loads after the prologue's LDS-DMA (counted vmcnt)
   rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
+  asm volatile("" ::: "memory");
   int* seq = reinterpret_cast<int*>(c.sRed + 2 * kRB);   // 2 partial buffers, seq words, row max
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) scene_pos_dma<NT>(a, c, fb, cnt);
-    scene_stage<NT>(
+    scene_stage<NT, TPW * 4>(
         a, lay, c, fb, cnt,
         [&] { if (fb == 0) rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L); },
         [&] {
@@ -1289,15 +1397,28 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) scene_pos_dma<NT>(a, c, fb, cnt);
-    scene_stage<NT>(a, lay, c, fb, cnt, [] {}, [] {});
+    scene_stage<NT, 0>(a, lay, c, fb, cnt, [] {}, [] {});
     load_item(fb, cnt, 0, tgA);       // first tiles' targets: in flight during the heads
     load_item(fb, cnt, 1, tgB);
+    // Rm = Wr @ Rel, Rel = Ve * Ve (train.py:194-195, g2k_lstm_mcr.py:106):
+    // rows t = 4q + i of column L, zero for t >= 8
+    float rm[4];
+    {
+      const float ve0 = c.sV[lay.wcmax * kD + L], ve1 = c.sV[(lay.wcmax + 1) * kD + L];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = 4 * q + i;
+        rm[i] = q < 2 ? fmaf(c.sm[SM_WR + 2 * t], ve0 * ve0, c.sm[SM_WR + 2 * t + 1] * (ve1 * ve1)) : 0.f;
+      }
+    }
     // phase 1 — the critical path: frame heads in frame order, As + M into
-    // the rings, then the frame's flag
+    // the rings, then the frame's flag; the first four frames' heads get the
+    // issue priority (the recurrence starts on them)
+    if (pw < 4) __builtin_amdgcn_s_setprio(1);
     for (int fl = pw; fl < cnt; fl += NP) {
       const int f = fb + fl;
       const FrameHeadOut hd =
-          frame_head(c.sm, c.sV + fl * stride * kD, c.sV + lay.wcmax * kD, c.sRing + fl * kD * kD,
+          frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, c.sRing + fl * kD * kD,
                      a.A_out ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
                      a.cost_out ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr, L, q);
       if (L < kL && q < 2) {
@@ -1308,6 +1429,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) *reinterpret_cast<volatile int*>(c.sFlag + fl) = f + 1;
       SSTAMP(3 + (f & 31), lane == 0);
+      __builtin_amdgcn_s_setprio(0);
     }
     // phase 2 — predictions and errors, tiles spread over all producers
 #ifdef G2K_DIAG_SKIP_TILES
@@ -1334,6 +1456,11 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     SSTAMP(80 + (c.wv & 15), lane == 0);
     __syncthreads();                                            // B3: chunk done
   }
+  if (pw == NP - 1) {
+    // frames beyond n_frames: zero predictions (off the critical path)
+    for (int i = lane; i < (F - c.nf) * kL2 * Nmax; i += 64)
+      a.pred[((size_t)s * F + c.nf) * kL2 * Nmax + i] = 0.f;
+  }
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     const float v = wave_sum(acc[k]);
@@ -1351,21 +1478,22 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.s = blockIdx.x;
   c.tid = threadIdx.x; c.lane = c.tid & 63; c.wv = c.tid >> 6; c.L = c.lane & 15; c.q = c.lane >> 4;
   const int Nmax = a.d.Nmax, F = a.d.F;
-  c.nact = clampi(a.n_active[c.s], 0, Nmax);
-  c.nf = a.n_frames ? clampi(a.n_frames[c.s], 0, F) : F;
   c.ntiles = (Nmax + 15) >> 4;
   c.sWi = smem + lay.o_wi; c.sWo = smem + lay.o_wo; c.sNrm = smem + lay.o_nrm; c.sV = smem + lay.o_v;
   c.sm = smem + lay.o_small; c.sMet = smem + lay.o_met; c.sRing = smem + lay.o_ring;
   c.sMring = smem + lay.o_mring; c.sRed = smem + lay.o_red; c.sPos = smem + lay.o_pos;
+  c.sVG = smem + lay.o_vg; c.sWig = smem + lay.o_wig;
   c.sY = smem + lay.o_y;
   c.sFlag = reinterpret_cast<int*>(smem + lay.o_flag);
   SSTAMP(0, c.tid == 0);
-  // frames beyond n_frames: zero predictions
-  for (int i = c.tid; i < (F - c.nf) * kL2 * Nmax; i += NT)
-    a.pred[((size_t)c.s * F + c.nf) * kL2 * Nmax + i] = 0.f;
-  if (c.nf > 0) {
+  if (F > 0) {
+    // issued before n_active / n_frames arrive: the first chunk's window for
+    // min(F, fc) frames (a scene with fewer frames reads rows it ignores)
     const int wv = c.wv, lane = c.lane, np = lay.np;
-    scene_pos_dma<NT>(a, c, 0, c.nf < lay.fc ? c.nf : lay.fc);   // critical path first
+#if !defined(G2K_DIAG_PROLOGUE) || G2K_DIAG_PROLOGUE != 2
+    scene_pos_dma<NT>(a, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
+#endif
+#if !defined(G2K_DIAG_PROLOGUE) || G2K_DIAG_PROLOGUE != 3
     dma4_copy_t<NT>(a.w.Wi, c.sWi, Nmax * kD, wv, lane);
     dma4_copy_t<NT>(a.w.Wo, c.sWo, kT * Nmax, wv, lane);
     dma4_copy_t<NT>(a.w.Wii, c.sm + SM_WII, kD * kT, wv, lane);
@@ -1377,13 +1505,24 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     const float* vis = a.vislet + (size_t)c.s * 2 * Nmax;
     dma4_copy_t<NT>(vis, c.sNrm + lay.wcmax * np, Nmax, wv, lane);
     dma4_copy_t<NT>(vis + Nmax, c.sNrm + (lay.wcmax + 1) * np, Nmax, wv, lane);
+#endif
     if (c.tid < kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;   // sequence words
     if (c.tid < lay.fc) c.sFlag[c.tid] = 0;              // flags hold (global frame + 1)
   }
+#ifdef G2K_DIAG_PROLOGUE
+  // diagnostic build only: the prologue's loads, one barrier, nothing else
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (c.tid == 0) a.metrics[c.s * 8] = smem[c.lane];
+  return;
+#endif
+  c.nact = clampi(a.n_active[c.s], 0, Nmax);
+  c.nf = a.n_frames ? clampi(a.n_frames[c.s], 0, F) : F;
   if (c.wv < kRecW)
     scene_recurrence<TPW, NP>(a, lay, c);
   else
     scene_producer<NP>(a, lay, c);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
   SSTAMP(100, c.tid == 0);
 }
 

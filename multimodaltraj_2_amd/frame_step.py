@@ -136,6 +136,36 @@ def step_fused(params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_fra
     targets [S, F, Nmax, L, 2], n_active [S] int32, h [S, D, H].
     ``F`` is taken from ``targets``.  Returns pred/h/metrics (and per-frame
     attn / cost when ``want_attn``)."""
+    plan = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
+                    ped_mask=ped_mask, stride=stride, lam=lam, out=out, want_attn=want_attn,
+                    stream=stream, h_out=h_out)
+    plan.run()
+    return plan.out
+
+
+class StepPlan:
+    """A validated launch of ``g2k_step_fused_f32`` bound to fixed device
+    buffers: the checks, the output allocation and the C argument list are
+    built once; ``run()`` is a single call across the C ABI on the bound
+    stream.  The buffers' contents may change between runs (that is how a
+    training loop feeds the next batch); their shapes and addresses may not."""
+
+    def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
+                 n_frames=None, ped_mask=None, stride=1, lam=LAMBDA,
+                 out: StepOutputs | None = None, want_attn=False, stream=None, h_out=None):
+        self._fn, self._args, self.out, self._keep = _prepare_step(
+            params, pos, vislet, G, targets, n_active, h, n_frames, ped_mask, stride, lam, out,
+            want_attn, stream, h_out)
+
+    def run(self) -> StepOutputs:
+        rc = self._fn(*self._args)
+        if rc:
+            _lib.check("g2k_step_fused_f32", rc)
+        return self.out
+
+
+def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_mask, stride, lam,
+                  out, want_attn, stream, h_out):
     lib = _lib.load()
     dev = pos.device
     if dev.type != "cuda":
@@ -178,13 +208,13 @@ def step_fused(params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_fra
     if nws < 0:
         _lib.check("g2k_step_workspace_bytes", -1)
     ws = _workspace(nws, dev)
-    rc = lib.g2k_step_fused_f32(ctypes.byref(d), ctypes.byref(w), _ptr(pos), _ptr(vislet),
-                                _ptr(G), _ptr(targets), _ptr(n_active), _ptr(n_frames),
-                                _ptr(ped_mask), _ptr(h), _ptr(out.h), _ptr(out.pred),
-                                _ptr(out.metrics), _ptr(out.attn), _ptr(out.cost),
-                                float(lam), ws.data_ptr(), nws, _stream(stream))
-    _lib.check("g2k_step_fused_f32", rc)
-    return out
+    args = (ctypes.byref(d), ctypes.byref(w), _ptr(pos), _ptr(vislet), _ptr(G), _ptr(targets),
+            _ptr(n_active), _ptr(n_frames), _ptr(ped_mask), _ptr(h), _ptr(out.h), _ptr(out.pred),
+            _ptr(out.metrics), _ptr(out.attn), _ptr(out.cost), ctypes.c_float(lam),
+            ws.data_ptr(), nws, _stream(stream))
+    # keep the tensors and ctypes structs the pointers refer to alive
+    keep = (d, w, params, pos, vislet, G, targets, n_active, n_frames, ped_mask, h, ws)
+    return lib.g2k_step_fused_f32, args, out, keep
 
 
 def mcr_forward(params: G2KParams, X, Rel, G, n_active, *, lam=LAMBDA, stream=None):

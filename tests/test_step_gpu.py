@@ -14,14 +14,14 @@ pytestmark = pytest.mark.gpu
 
 
 def run_both(S, Nmax, H, F=20, seed=1, n_active=None, h0_scale=0.0, ped_mask=None,
-             n_frames=None, device=None):
+             n_frames=None, device=None, lam=fs.LAMBDA):
     b = make_batch(S, Nmax, H, F=F, seed=seed, n_active=n_active, h0_scale=h0_scale)
     params = fs.init_params(Nmax, seed=0, device=device)
     t = b.to_device(device)
     pm = None if ped_mask is None else torch.from_numpy(ped_mask.astype(np.uint8)).to(device)
     nfr = None if n_frames is None else torch.from_numpy(np.asarray(n_frames, np.int32)).to(device)
     out = fs.step_fused(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
-                        t["h0"], n_frames=nfr, ped_mask=pm, stride=1, want_attn=True)
+                        t["h0"], n_frames=nfr, ped_mask=pm, stride=1, want_attn=True, lam=lam)
     torch.cuda.synchronize()
     w = params.numpy()
     res = []
@@ -30,7 +30,7 @@ def run_both(S, Nmax, H, F=20, seed=1, n_active=None, h0_scale=0.0, ped_mask=Non
         pr, h, m, ex = ref.scene_step(b.pos[s], b.vislet[s], b.G[s], w, b.targets[s],
                                       b.n_active[s], b.h0[s], n_frames=nf, stride=1,
                                       ped_mask=None if ped_mask is None else ped_mask[s],
-                                      keep=True)
+                                      keep=True, lam=lam)
         res.append((pr, h, m, ex))
     return b, out, res
 
@@ -58,6 +58,24 @@ def test_step_matches_oracle(gpu, S, Nmax, H):
         assert close(cost[s], np.stack(ex["cost"])) <= TOL
         assert close(hh[s], h) <= TOL
         assert close(met[s, :6], m[:6]) <= TOL
+
+
+def test_step_large_logits(gpu):
+    """lambda = 0.1 puts |A| up to ~160 with column spreads > 87, where
+    exp(A - column max) underflows: the running-max fallback of the As step
+    (train.py:240) must take over (the float64 oracle is exact there)."""
+    b, out, res = run_both(3, 32, 64, F=12, device=gpu, lam=0.1)
+    hh = out.h.cpu().numpy()
+    attn = out.attn.cpu().numpy()
+    pred = out.pred.cpu().numpy()
+    for s in range(3):
+        n = int(b.n_active[s])
+        pr, h, m, ex = res[s]
+        A_ref = np.stack(ex["A"])
+        assert np.abs(A_ref).max() > 87.0
+        assert np.abs(attn[s] - A_ref).max() <= TOL * max(1.0, np.abs(A_ref).max())
+        assert close(pred[s, :, :, :n].reshape(12, 2, 12, n), pr) <= TOL
+        assert close(hh[s], h) <= TOL
 
 
 def test_step_nonzero_h0_and_masks(gpu):
