@@ -84,6 +84,11 @@ __device__ unsigned long long g2k_sstamps[4][128];
 
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
+// The wave's index in its workgroup, provably wave-uniform (an SGPR): role
+// branches, per-wave loops and s_setprio guards on it compile to scalar
+// branches instead of exec-masked code.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 
 // LDS-DMA: 16 bytes per lane, LDS destination = wave-uniform base + 16*lane.
 __device__ __forceinline__ void dma16(const float* gsrc, float* lds_wave_base) {
@@ -258,6 +263,9 @@ __device__ __forceinline__ void attn_row_pass(float* A, int r, float* gout) {
 // yields wrong numbers, not a hung GPU.
 // ---------------------------------------------------------------------------
 constexpr int kPollMax = 1 << 20;
+#ifndef G2K_DIAG_TILE
+#define G2K_DIAG_TILE 0   // diagnostic builds only: 1 no errors, 2 no pred stores, 4 no MFMA
+#endif
 #ifndef G2K_POLL_SLEEP
 #define G2K_POLL_SLEEP 1
 #endif
@@ -272,41 +280,46 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 
 
 
-// One frame's inputs of the recurrence in one LDS round trip: the 4
-// recurrence waves' sequence words (seq[w] = frames whose row partials wave w
-// has published, +1), the producer's flag of this frame's As tile, the As row
-// quad and the row partials of the 4 waves.  Each writer stores its data
-// before its word, and the words are read before the data, so seeing
-// min(seq) >= want_seq and flag == want_flag means the data read is current.
-// Busy poll for the first rounds (the scene's critical path), then s_sleep.
-__device__ __forceinline__ void poll_frame(const int* seq, int want_seq, const int* flag,
-                                           int want_flag, const float* asrc, const float* rsrc,
+// One frame's inputs of the recurrence in one LDS round trip.  Lane (L, q)
+// reads ONE recurrence wave's row-partial quad (wave w = L & 3, rows
+// 4q..4q+3) and that wave's sequence word (seq[w] = frames whose partials w
+// has published, +1), the producer's flag of this frame's As tile and the As
+// row quad; the four waves' quads are then summed across each lane quad by
+// DPP.  Each writer stores its data before its word and the words are read
+// before the data, so every lane seeing seq >= want_seq and flag == want_flag
+// means all data read is current.  Busy poll for the first rounds (the
+// scene's critical path), then s_sleep.
+__device__ __forceinline__ void poll_frame(const int* seq_w, int want_seq, const int* flag,
+                                           int want_flag, const float* asrc, const float* rslot,
                                            float4& b, float4& z) {
-  const uint32_t sa = lds_addr(seq), fa = lds_addr(flag), da = lds_addr(asrc), ra = lds_addr(rsrc);
-  int fl;
-  i32x4 sq;
-  f32x4 v, a0, a1, a2, a3;
+  const uint32_t sa = lds_addr(seq_w), fa = lds_addr(flag), da = lds_addr(asrc), ra = lds_addr(rslot);
+  int sq, fl;
+  f32x4 v, r;
   for (int it = 0; it < kPollMax; ++it) {
     asm volatile(
-        "ds_read_b128 %0, %7\n\t"
-        "ds_read_b32 %1, %8\n\t"
-        "ds_read_b128 %2, %9\n\t"
-        "ds_read_b128 %3, %10\n\t"
-        "ds_read_b128 %4, %10 offset:64\n\t"
-        "ds_read_b128 %5, %10 offset:128\n\t"
-        "ds_read_b128 %6, %10 offset:192\n\t"
+        "ds_read_b32 %0, %4\n\t"
+        "ds_read_b32 %1, %5\n\t"
+        "ds_read_b128 %2, %6\n\t"
+        "ds_read_b128 %3, %7\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&v"(sq), "=&v"(fl), "=&v"(v), "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+        : "=&v"(sq), "=&v"(fl), "=&v"(v), "=&v"(r)
         : "v"(sa), "v"(fa), "v"(da), "v"(ra)
         : "memory");
-    const int smin = min(min(__builtin_amdgcn_readfirstlane(sq[0]), __builtin_amdgcn_readfirstlane(sq[1])),
-                         min(__builtin_amdgcn_readfirstlane(sq[2]), __builtin_amdgcn_readfirstlane(sq[3])));
-    if (smin >= want_seq && __builtin_amdgcn_readfirstlane(fl) == want_flag) break;
+    if (__builtin_amdgcn_ballot_w64(sq < want_seq) == 0 &&
+        __builtin_amdgcn_readfirstlane(fl) == want_flag)
+      break;
     if (it >= 8) __builtin_amdgcn_s_sleep(1);   // long waits (the first heads): back off
   }
   b = make_float4(v[0], v[1], v[2], v[3]);
-  z = make_float4(((a0[0] + a1[0]) + a2[0]) + a3[0], ((a0[1] + a1[1]) + a2[1]) + a3[1],
-                  ((a0[2] + a1[2]) + a2[2]) + a3[2], ((a0[3] + a1[3]) + a2[3]) + a3[3]);
+  float zz[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float t = r[i];
+    t += dpp<0xB1>(t);   // quad_perm [1,0,3,2]
+    t += dpp<0x4E>(t);   // quad_perm [2,3,0,1]
+    zz[i] = t;
+  }
+  z = make_float4(zz[0], zz[1], zz[2], zz[3]);
 }
 
 // Wait until a frame flag reaches `want` (no data attached).
@@ -574,7 +587,7 @@ __device__ __forceinline__ void lse_combine(float& m, float& s, float m2, float 
 __global__ void __launch_bounds__(kNT) g2k_frames_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int chunk = blockIdx.x, s = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, L = lane & 15, q = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), L = lane & 15, q = lane >> 4;
   const int Nmax = a.d.Nmax, W = a.d.W, F = a.d.F, stride = a.d.stride;
   const int nact = clampi(a.n_active[s], 0, Nmax);
   const int nf = a.n_frames ? clampi(a.n_frames[s], 0, F) : F;
@@ -882,7 +895,7 @@ __global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(RecurArgs a) {
   __shared__ __attribute__((aligned(16))) float sAs[kRecurChunk * kD * kD];
   __shared__ __attribute__((aligned(16))) float sRed[4 * kRB];
   const int s = blockIdx.x, tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6, q = lane >> 4, j = lane & 15;
+  const int lane = tid & 63, wv = wave_id(), q = lane >> 4, j = lane & 15;
   const int F = a.F, H = a.H;
   const int nf = a.n_frames ? clampi(a.n_frames[s], 0, F) : F;
   STAMP(10);
@@ -1157,11 +1170,16 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
     const float wo = n < nact ? sWo[k * Nmax + n] : 0.f;
     const float bx = L < kL ? M[L * kT + k] : 0.f;
     const float by = L < kL ? M[(kL + L) * kT + k] : 0.f;
+#if (G2K_DIAG_TILE & 4)
+    y0[ks] = wo * bx; y1[ks] = wo * by;   // diagnostic build only
+#else
     y0 = mfma4(wo, bx, y0);   // Y[L][n0 + 4q + i]
     y1 = mfma4(wo, by, y1);   // Y[12 + L][n0 + 4q + i]
+#endif
   }
   if (L < kL) {
     const int nb = n0 + 4 * q;
+#if !(G2K_DIAG_TILE & 2)
     if (nb + 3 < Nmax && ((Nmax & 3) == 0)) {
       *reinterpret_cast<float4*>(pr + L * Nmax + nb) = make_float4(y0[0], y0[1], y0[2], y0[3]);
       *reinterpret_cast<float4*>(pr + (kL + L) * Nmax + nb) = make_float4(y1[0], y1[1], y1[2], y1[3]);
@@ -1170,10 +1188,14 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
       for (int i = 0; i < 4; ++i)
         if (nb + i < Nmax) { pr[L * Nmax + nb + i] = y0[i]; pr[(kL + L) * Nmax + nb + i] = y1[i]; }
     }
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       *reinterpret_cast<float2*>(ys + (4 * q + i) * kL2 + 2 * L) = make_float2(y0[i], y1[i]);
   }
+#if (G2K_DIAG_TILE & 1)
+  return;   // diagnostic build only
+#endif
   __builtin_amdgcn_wave_barrier();
   float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f, fx = 0.f, fy = 0.f;
   const float2* yp = reinterpret_cast<const float2*>(ys + pp * kL2) + 3 * u;
@@ -1347,8 +1369,9 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     for (int fl = 0; fl < cnt; ++fl) {
       const int g = fb + fl;                 // global frame index
       float4 b, z;
-      poll_frame(seq, g + 1, c.sFlag + fl, g + 1, c.sRing + fl * kD * kD + c.L * kD + 4 * c.q,
-                 c.sRed + (g & 1) * kRB + 4 * c.q, b, z);
+      poll_frame(seq + (c.L & 3), g + 1, c.sFlag + fl, g + 1,
+                 c.sRing + fl * kD * kD + c.L * kD + 4 * c.q,
+                 c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, b, z);
       rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 2, c.wv, c.q, c.L);
       SSTAMP(40 + ((fb + fl) & 31), c.tid == 0);
     }
@@ -1476,7 +1499,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   extern __shared__ __attribute__((aligned(16))) float smem[];
   SceneCtx c;
   c.s = blockIdx.x;
-  c.tid = threadIdx.x; c.lane = c.tid & 63; c.wv = c.tid >> 6; c.L = c.lane & 15; c.q = c.lane >> 4;
+  c.tid = threadIdx.x; c.lane = c.tid & 63; c.wv = wave_id(); c.L = c.lane & 15; c.q = c.lane >> 4;
   const int Nmax = a.d.Nmax, F = a.d.F;
   c.ntiles = (Nmax + 15) >> 4;
   c.sWi = smem + lay.o_wi; c.sWo = smem + lay.o_wo; c.sNrm = smem + lay.o_nrm; c.sV = smem + lay.o_v;
@@ -1494,21 +1517,34 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     scene_pos_dma<NT>(a, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
 #endif
 #if !defined(G2K_DIAG_PROLOGUE) || G2K_DIAG_PROLOGUE != 3
-    dma4_copy_t<NT>(a.w.Wi, c.sWi, Nmax * kD, wv, lane);
-    dma4_copy_t<NT>(a.w.Wo, c.sWo, kT * Nmax, wv, lane);
-    dma4_copy_t<NT>(a.w.Wii, c.sm + SM_WII, kD * kT, wv, lane);
-    dma4_copy_t<NT>(a.G + (size_t)c.s * kD * kT, c.sm + SM_G, kD * kT, wv, lane);
-    dma4_copy_t<NT>(a.w.Wv, c.sm + SM_WV, kT * (kD + 2), wv, lane);
-    dma4_copy_t<NT>(a.w.bv, c.sm + SM_BV, kD, wv, lane);
-    dma4_copy_t<NT>(a.w.Wr, c.sm + SM_WR, kT * 2, wv, lane);
-    dma4_copy_t<NT>(a.w.Wc, c.sm + SM_WC, kL2 * kT, wv, lane);
-    const float* vis = a.vislet + (size_t)c.s * 2 * Nmax;
-    dma4_copy_t<NT>(vis, c.sNrm + lay.wcmax * np, Nmax, wv, lane);
-    dma4_copy_t<NT>(vis + Nmax, c.sNrm + (lay.wcmax + 1) * np, Nmax, wv, lane);
+    // the small segments: one wave each (one pointer per wave keeps the
+    // kernel-argument loads off a serial s_load / s_waitcnt chain)
+    for (int seg = wv; seg < 10; seg += NT / 64) {
+      const float* src;
+      float* dst;
+      int n;
+      switch (seg) {
+        case 0: src = a.w.Wi; dst = c.sWi; n = Nmax * kD; break;
+        case 1: src = a.w.Wo; dst = c.sWo; n = kT * Nmax; break;
+        case 2: src = a.w.Wii; dst = c.sm + SM_WII; n = kD * kT; break;
+        case 3: src = a.G + (size_t)c.s * kD * kT; dst = c.sm + SM_G; n = kD * kT; break;
+        case 4: src = a.w.Wv; dst = c.sm + SM_WV; n = kT * (kD + 2); break;
+        case 5: src = a.w.bv; dst = c.sm + SM_BV; n = kD; break;
+        case 6: src = a.w.Wr; dst = c.sm + SM_WR; n = kT * 2; break;
+        case 7: src = a.w.Wc; dst = c.sm + SM_WC; n = kL2 * kT; break;
+        case 8: src = a.vislet + (size_t)c.s * 2 * Nmax; dst = c.sNrm + lay.wcmax * np; n = Nmax; break;
+        default: src = a.vislet + (size_t)c.s * 2 * Nmax + Nmax; dst = c.sNrm + (lay.wcmax + 1) * np; n = Nmax; break;
+      }
+      for (int i = 0; i < n; i += 64)
+        if (i + lane < n)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i + lane),
+                                           (__attribute__((address_space(3))) void*)(dst + i), 4, 0, 0);
+    }
 #endif
     if (c.tid < kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;   // sequence words
     if (c.tid < lay.fc) c.sFlag[c.tid] = 0;              // flags hold (global frame + 1)
   }
+  SSTAMP(103, c.tid == 0);
 #ifdef G2K_DIAG_PROLOGUE
   // diagnostic build only: the prologue's loads, one barrier, nothing else
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1518,6 +1554,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
 #endif
   c.nact = clampi(a.n_active[c.s], 0, Nmax);
   c.nf = a.n_frames ? clampi(a.n_frames[c.s], 0, F) : F;
+  SSTAMP(104, c.tid == 0 && c.nf >= 0);
   if (c.wv < kRecW)
     scene_recurrence<TPW, NP>(a, lay, c);
   else
@@ -1610,7 +1647,7 @@ struct ErrArgs {
 
 __global__ void __launch_bounds__(kNT) g2k_errors_v0_kernel(ErrArgs a) {
   __shared__ float sMet[32];
-  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = wave_id();
   const int Nmax = a.d.Nmax, F = a.d.F;
   int nact = a.n_active[s];
   nact = nact < 0 ? 0 : (nact > Nmax ? Nmax : nact);
@@ -1782,11 +1819,11 @@ int launch_recur(const RecurArgs& r, int S, hipStream_t st) {
 
 // Fused scene kernel geometry: producer waves (NP) and the frames-per-chunk
 // that fits LDS.  NP = 8 by default (12 waves: one recurrence + two producer
-// waves per SIMD); G2K_SCENE_NP in {4, 8, 12} is a tuning override.
+// waves per SIMD); G2K_SCENE_NP in {4, 6, 8, 12} is a tuning override.
 int scene_producers(int H) {
   int np = 8;
   const char* env = getenv("G2K_SCENE_NP");
-  if (env && (atoi(env) == 4 || atoi(env) == 8 || atoi(env) == 12)) np = atoi(env);
+  if (env && (atoi(env) == 4 || atoi(env) == 6 || atoi(env) == 8 || atoi(env) == 12)) np = atoi(env);
   if (H >= 512) np = 4;            // TPW 8 needs > 128 VGPRs: at most 512 threads
   return np;
 }
@@ -1827,6 +1864,7 @@ int launch_scene(const StepArgs& a, const SceneLayout& l, int NP, hipStream_t st
   }
   switch (NP) {
     case 4: return launch_scene_np<4>(a, l, st);
+    case 6: return launch_scene_np<6>(a, l, st);
     case 8: return launch_scene_np<8>(a, l, st);
     case 12: return launch_scene_np<12>(a, l, st);
     default: return set_err(G2K_EUNSUPPORTED, "NP=%d", NP);

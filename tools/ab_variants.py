@@ -51,13 +51,15 @@ def main():
             os.environ.update(env)
             _lib._lib = lib
             try:
+                plan = fs.StepPlan(p, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+                o = plan.out
                 for _ in range(3):
-                    o = fs.step_fused(p, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+                    plan.run()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
                 e0.record()
                 for _ in range(50):
-                    fs.step_fused(p, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"], out=o)
+                    plan.run()
                 e1.record()
                 torch.cuda.synchronize()
                 res[name].append(e0.elapsed_time(e1) / 50 * 1e3)

@@ -9,8 +9,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from multimodaltraj_2_amd import _lib, build, frame_step as fs
 from multimodaltraj_2_amd.synthetic import make_batch, CONFIGS
 
+extra = [f for f in os.environ.get("G2K_DIAG_FLAGS", "").split(",") if f]
 out = "/tmp/libg2k_sstamps.so"
-subprocess.run([build.HIPCC, *build.FLAGS, "-DG2K_STAMPS_SCENE", "-o", out, *build.SRC], check=True)
+subprocess.run([build.HIPCC, *build.FLAGS, "-DG2K_STAMPS_SCENE", *extra, "-o", out, *build.SRC],
+               check=True)
 lib = _lib.load(out)
 _lib._lib = lib
 lib.g2k_debug_sstamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
@@ -34,7 +36,7 @@ for k in range(4):
     if blk >= S:
         continue
     r = v[k] - t0
-    print(f"== WG {blk} n_active={b.n_active[blk]}: start {r[0]} vmcnt {r[102]} B1 {r[1]} B1b {r[101]} B2 {r[2]} end {r[100]}")
+    print(f"== WG {blk} n_active={b.n_active[blk]}: start {r[0]} dma-issued {r[103]} nf-known {r[104]} vmcnt {r[102]} B1 {r[1]} B1b {r[101]} B2 {r[2]} end {r[100]}")
     print("   producer flags:", " ".join(str(x) for x in r[3:3 + F]))
     print("   recur done    :", " ".join(str(x) for x in r[40:40 + F]))
     print("   recur per-frame:", " ".join(str(x) for x in np.diff(r[40:40 + F])))
