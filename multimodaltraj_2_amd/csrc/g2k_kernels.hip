@@ -322,6 +322,17 @@ __device__ __forceinline__ void poll_frame(const int* seq_w, int want_seq, const
   z = make_float4(zz[0], zz[1], zz[2], zz[3]);
 }
 
+// Wait until every lane's sequence word (lane L reads seq_w = seq + (L & 3))
+// reaches `want`.
+__device__ __forceinline__ void poll_seq(const int* seq_w, int want) {
+  const uint32_t sa = lds_addr(seq_w);
+  int sq;
+  for (int it = 0; it < kPollMax; ++it) {
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(sq) : "v"(sa) : "memory");
+    if (__builtin_amdgcn_ballot_w64(sq < want) == 0) break;
+  }
+}
+
 // Wait until a frame flag reaches `want` (no data attached).
 __device__ __forceinline__ void poll_flag(const int* flag, int want) {
   const uint32_t fa = lds_addr(flag);
@@ -965,17 +976,15 @@ constexpr int kSceneChunk = 32;
 constexpr int kRecW = 4;
 // scene-kernel small block: the split path's offsets plus weight-derived
 // matrices (DESIGN.md "frame head"): K1 = [Wv16 @ Wii | Wv16.. | Wv17.. | 1 | 0]
-// ([8][12]), K2 = Wc @ K1 ([24][12]), bvg = bv @ g ([8]).
+// ([8][12]), K2 = Wc @ K1 ([24][12]).  G stays unscaled (lambda applied at use).
 constexpr int SM_K1 = 640;
-constexpr int SM_BVG = 736;
 constexpr int SM_K2 = 752;
 constexpr int kSceneSmall = 1088;
 constexpr int kKA = 12;        // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
 
 struct SceneLayout {
-  int fc, wcmax, np;
-  int o_wi, o_wo, o_nrm, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_red, o_pos, o_vg,
-      o_wig;
+  int fc, wcmax, pp;   // frames per chunk, window rows per chunk, pos row pitch (floats)
+  int o_wi, o_wo, o_vis, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_red, o_pos, o_vg;
   int total;   // floats
 };
 
@@ -983,26 +992,27 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   SceneLayout s;
   s.fc = fc;
   s.wcmax = (fc - 1) * stride + kT;
-  s.np = Nmax + 1;
+  s.pp = 2 * Nmax + 4;                        // padded rows: lanes reading across rows spread banks
   int o = 0;
   s.o_wi = o;    o += rup4(Nmax * kD);
   s.o_wo = o;    o += rup4(kT * Nmax);
-  s.o_nrm = o;   o += rup4((s.wcmax + 2) * s.np);
-  s.o_v = o;     o += rup4((s.wcmax + 2) * kD);
+  s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
+  s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
   s.o_y = o;     o += NP * kD * kL2;
   s.o_met = o;   o += NP * 8;
-  s.o_vg = o;    o += rup4((s.wcmax + 2) * kT);    // VG = V @ g rows (window + vislet)
-  s.o_wig = o;   o += rup4(Nmax * kT);             // Wig = Wi @ g
   s.o_ring = o;  o += fc * kD * kD;
-  s.o_mring = o; o += fc * kL2 * kT;         // M = Wc @ cost per frame [24][8]
+  s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
   s.o_flag = o;  o += rup4(fc);
   s.o_red = o;   o += 4 * 16 * kRecW;
-  s.o_pos = o;   o += rup4(s.wcmax * Nmax * 2);   // raw position window (LDS-DMA)
+  s.o_pos = o;   o += s.wcmax * s.pp;                  // raw position window (LDS-DMA)
+  s.o_vg = o;    o += rup4((s.wcmax + 3) * kT);       // VG = V @ g: window, Ve0, Ve1, bv rows
   s.total = o;
   return s;
 }
 
+// frame head output: the x / y row tiles of M^T
+// frame head output: the x / y row tiles of M^T
 struct FrameHeadOut {
   f32x4 mT0, mT1;   // M[L][4q+i] (x rows), M[12+L][4q+i] (y rows)
 };
@@ -1096,7 +1106,7 @@ __device__ __forceinline__ void attn_weights(const f32x4 aA, float* as_dst, int 
 // As goes to `as_dst`; the x / y row tiles of M^T are returned (M[L][4q+i]).
 __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float* sV,
                                                    const float* sVG, int wrow0, int wcmax,
-                                                   const float (&rm)[4], float* as_dst,
+                                                   const float (&rm)[4], float lam, float* as_dst,
                                                    float* A_g, float* cost_g, int L, int q) {
   float ka[3], ua[3], va[3];
 #pragma unroll
@@ -1108,7 +1118,7 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
       va[ks] = L < kT ? sVG[(wrow0 + k) * kT + L] : 0.f;
     } else {
       ua[ks] = q < 2 ? sV[(wcmax + q) * kD + L] : (q == 2 ? sm[SM_BV + L] : 0.f);
-      va[ks] = L >= kT ? 0.f : (q < 2 ? sVG[(wcmax + q) * kT + L] : (q == 2 ? sm[SM_BVG + L] : 0.f));
+      va[ks] = L >= kT || q == 3 ? 0.f : sVG[(wcmax + q) * kT + L];   // Ve0, Ve1, bv rows
     }
   }
   f32x4 eN = {0.f, 0.f, 0.f, 0.f};
@@ -1131,7 +1141,7 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
   f32x4 aA = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    const float gA = q < 2 ? sm[SM_G + L * kT + 4 * q + ks] : 0.f;       // g[r = L][t]
+    const float gA = q < 2 ? lam * sm[SM_G + L * kT + 4 * q + ks] : 0.f;  // g[r = L][t]
     aA = mfma4(gA, em[ks], aA);                                          // A[4q+i][L]
   }
   if (A_g) {
@@ -1230,35 +1240,166 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
 
 // Per-workgroup context of the scene kernel (LDS carve-up, scene scalars).
 struct SceneCtx {
-  float *sWi, *sWo, *sNrm, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sY, *sPos, *sVG, *sWig;
+  float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sY, *sPos, *sVG;
   int* sFlag;
   int s, tid, lane, wv, L, q, nact, nf, ntiles;
 };
 
-// LDS-DMA of a chunk's position window rows (train.py:76-79 window).
+// LDS-DMA of a chunk's position window rows (train.py:76-79 window) into
+// rows of pitch lay.pp: wave w issues rows w, w + waves, ...
 template <int NT>
-__device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneCtx& c, int fb, int cnt) {
+__device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneLayout& lay,
+                                              const SceneCtx& c, int fb, int cnt) {
   const int Nmax = a.d.Nmax, stride = a.d.stride;
   const int wcc = (cnt - 1) * stride + kT;
   const float* src = a.pos + ((size_t)c.s * a.d.W + fb * stride) * Nmax * 2;
-  if ((Nmax & 1) == 0 && (((uintptr_t)a.pos) & 15) == 0)
-    dma_copy_n<NT>(src, c.sPos, wcc * Nmax / 2, c.wv, c.lane);      // 16-B granules
-  else
-    dma4_copy_t<NT>(src, c.sPos, wcc * Nmax * 2, c.wv, c.lane);
+  const bool wide = (Nmax & 1) == 0 && (((uintptr_t)a.pos) & 15) == 0;
+  for (int r = c.wv; r < wcc; r += NT / 64) {
+    const float* g = src + (size_t)r * Nmax * 2;
+    float* d = c.sPos + r * lay.pp;
+    if (wide) {
+      for (int i = 0; i < Nmax / 2; i += 64)
+        if (i + c.lane < Nmax / 2) dma16(g + 4 * (i + c.lane), d + 4 * i);
+    } else {
+      for (int i = 0; i < 2 * Nmax; i += 64)
+        if (i + c.lane < 2 * Nmax)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + i + c.lane),
+                                           (__attribute__((address_space(3))) void*)(d + i), 4, 0, 0);
+    }
+  }
 }
 
-// Chunk staging shared by both roles (every thread takes part).  The chunk's
-// position window is already in flight by LDS-DMA (scene_pos_dma).  Wait,
-// barrier; window norms ||(x, y)||_2 (train.py:79) into sNrm, barrier; V =
-// norms @ Wi for the chunk's window rows (train.py:179) and the two vislet
-// rows (Ve), barrier.  `mid1` runs before the second barrier, `mid2` before
-// the third.
-template <int NT, int VMC, typename Mid1, typename Mid2>
+// One 16-row tile of the chunk's embedding rows, by MFMA (train.py:76-79,
+// 167-195): local rows r = w0 + L are the window rows (r < wcc: norms
+// ||pos||, formed here from the LDS window), the two vislet rows and a bv
+// pseudo-row (VG only).  V^T = Wi^T @ N^T over n (k = 4 ks + q), then
+// VG^T = (lambda G)^T @ V^T over d with V^T straight from the registers.
+// Lane (L, q) ends with V[r][4q..4q+3] and VG[r][4q..4q+3] (q < 2).
+__device__ __forceinline__ void scene_vtile(const StepArgs& a, const SceneLayout& lay,
+                                            const SceneCtx& c, int w0, int wcc) {
+  // branch-free: every lane loads at clamped addresses and selects, so the
+  // LDS reads of several k-steps are in flight together
+  const int Nmax = a.d.Nmax, L = c.L, q = c.q, nact = c.nact;
+  const int r = w0 + L;
+  const bool win = r < wcc, vis = r >= wcc && r < wcc + 2, bvrow = r == wcc + 2;
+  const float* prow = c.sPos + (win ? r : 0) * lay.pp;
+  const float* vrow = c.sVis + (vis ? r - wcc : 0) * Nmax;
+  struct Raw { float wi, px, py, v; };
+  auto load = [&](int ks) {
+    const int n = 4 * ks + q;
+    const int nc = n < Nmax ? n : Nmax - 1;
+    const float2 p = *reinterpret_cast<const float2*>(prow + 2 * nc);
+    return Raw{c.sWi[nc * kD + L], p.x, p.y, vrow[nc]};           // Wi[n][d = L], pos, vislet
+  };
+  auto value = [&](int ks, const Raw& w) {                         // N[w0 + L][n]
+    const int n = 4 * ks + q;
+    const float nrm = __builtin_amdgcn_sqrtf(fmaf(w.px, w.px, w.py * w.py));
+    return n < nact ? (win ? nrm : (vis ? w.v : 0.f)) : 0.f;
+  };
+  const int nks = (Nmax + 3) / 4;
+  f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+  SSTAMP(114, c.lane == 0 && w0 == 0);
+  int ks = 0;
+  for (; ks + 4 <= nks; ks += 4) {
+    Raw r0 = load(ks), r1 = load(ks + 1), r2 = load(ks + 2), r3 = load(ks + 3);
+    // keep all twelve loads unconditional and in flight together
+    asm volatile("" : "+v"(r0.wi), "+v"(r0.px), "+v"(r0.py), "+v"(r0.v), "+v"(r1.wi), "+v"(r1.px),
+                 "+v"(r1.py), "+v"(r1.v), "+v"(r2.wi), "+v"(r2.px), "+v"(r2.py), "+v"(r2.v),
+                 "+v"(r3.wi), "+v"(r3.px), "+v"(r3.py), "+v"(r3.v));
+    v0 = mfma4(r0.wi, value(ks, r0), v0);                          // V[w0 + L][4q + i]
+    v1 = mfma4(r1.wi, value(ks + 1, r1), v1);
+    v0 = mfma4(r2.wi, value(ks + 2, r2), v0);
+    v1 = mfma4(r3.wi, value(ks + 3, r3), v1);
+  }
+  for (; ks < nks; ++ks) {
+    Raw r0 = load(ks);
+    asm volatile("" : "+v"(r0.wi), "+v"(r0.px), "+v"(r0.py), "+v"(r0.v));
+    v0 = mfma4(r0.wi, value(ks, r0), v0);
+  }
+  f32x4 vt;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) vt[i] = v0[i] + v1[i];
+  SSTAMP(115, c.lane == 0 && w0 == 0);
+  f32x4 vg = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks2 = 0; ks2 < 4; ++ks2) {
+    const float gl = c.sm[SM_G + (4 * q + ks2) * kT + (L & 7)];
+    const float ga = L < kT ? a.lambda * gl : 0.f;                          // g[d][t2 = L]
+    const float bvv = c.sm[SM_BV + 4 * q + ks2];
+    vg = mfma4(ga, bvrow ? bvv : vt[ks2], vg);                             // VG[w0 + L][4q + i]
+  }
+  const int row = win ? r : lay.wcmax + (r - wcc);               // storage row
+  if (win || vis)
+    *reinterpret_cast<float4*>(c.sV + row * kD + 4 * q) = make_float4(vt[0], vt[1], vt[2], vt[3]);
+  if ((win || vis || bvrow) && q < 2)
+    *reinterpret_cast<float4*>(c.sVG + row * kT + 4 * q) = make_float4(vg[0], vg[1], vg[2], vg[3]);
+}
+
+// K1 = [Wv[:, :16] @ Wii | Wv[:, 16] | Wv[:, 17] | 1 | 0] ([8][12]) and
+// K2 = Wc @ K1 ([24][12]) by MFMA in one wave (weights only; see frame_head).
+__device__ __forceinline__ void scene_kmats(const SceneCtx& c) {
+  const int L = c.L, q = c.q, L7 = L & 7;
+  const float* sm = c.sm;
+  float av[4], bw[4];
+  float wv16[4], wv17[4], wc0[4], wc1[4];
+  const int q1 = q & 1;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int d = 4 * q + ks;
+    av[ks] = sm[SM_WV + L7 * (kD + 2) + d];                      // Wv[t = L][d]
+    bw[ks] = sm[SM_WII + d * kT + L7];                           // Wii[d][k = L]
+    const int t = 4 * q1 + ks;
+    wv16[ks] = sm[SM_WV + t * (kD + 2) + kD];
+    wv17[ks] = sm[SM_WV + t * (kD + 2) + kD + 1];
+    wc0[ks] = sm[SM_WC + L * kT + 4 * q1 + ks];                 // Wc rows 0..15
+    wc1[ks] = sm[SM_WC + (16 + L7) * kT + 4 * q1 + ks];        // Wc rows 16..23
+  }
+  asm volatile("" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(bw[0]), "+v"(bw[1]),
+               "+v"(bw[2]), "+v"(bw[3]));
+  asm volatile("" : "+v"(wc0[0]), "+v"(wc0[1]), "+v"(wc0[2]), "+v"(wc0[3]), "+v"(wc1[0]),
+               "+v"(wc1[1]), "+v"(wc1[2]), "+v"(wc1[3]));
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    av[ks] = L < kT ? av[ks] : 0.f;
+    bw[ks] = L < kT ? bw[ks] : 0.f;
+    wc0[ks] = q < 2 ? wc0[ks] : 0.f;
+    wc1[ks] = (q < 2 && L < kL2 - 16) ? wc1[ks] : 0.f;
+  }
+  f32x4 k1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) k1 = mfma4(av[ks], bw[ks], k1);   // K1[4q + i][L]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v = k1[i];
+    v = L == 8 ? wv16[i] : L == 9 ? wv17[i] : L == 10 ? 1.f : L == 11 ? 0.f : v;
+    k1[i] = (q < 2 && L < kKA) ? v : 0.f;
+  }
+  f32x4 ka = {0.f, 0.f, 0.f, 0.f}, kb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    ka = mfma4(wc0[ks], k1[ks], ka);                               // K2[4q + i][L]
+    kb = mfma4(wc1[ks], k1[ks], kb);                               // K2[16 + 4q + i][L]
+  }
+  if (L < kKA) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 4 * q + i;
+      if (q < 2) c.sm[SM_K1 + t * kKA + L] = k1[i];
+      c.sm[SM_K2 + t * kKA + L] = ka[i];
+      if (16 + t < kL2) c.sm[SM_K2 + (16 + t) * kKA + L] = kb[i];
+    }
+  }
+}
+
+// Chunk staging shared by both roles (every wave takes part).  The chunk's
+// position window is in flight by LDS-DMA (scene_pos_dma).  Wait, barrier;
+// the producer waves compute the embedding-row tiles (scene_vtile) and, at
+// the first chunk, K1 / K2 (scene_kmats) while `rec_init` runs on the
+// recurrence waves; barrier.
+template <int NT, int NP, int VMC, typename RecInit>
 __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout& lay,
-                                            const SceneCtx& c, int fb, int cnt, Mid1 mid1,
-                                            Mid2 mid2) {
-  const int Nmax = a.d.Nmax, stride = a.d.stride, np = lay.np;
-  const int wcc = (cnt - 1) * stride + kT;
+                                            const SceneCtx& c, int fb, int cnt, RecInit rec_init) {
+  const int wcc = (cnt - 1) * a.d.stride + kT;
   // VMC = vector-memory ops this wave issued after the LDS-DMA that may stay
   // in flight (the recurrence's h loads at the first chunk)
   if (VMC > 0 && fb == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
@@ -1266,78 +1407,21 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
   SSTAMP(102, c.tid == 0 && fb == 0);
   __syncthreads();                                              // B1: window + weights landed
   SSTAMP(1, c.tid == 0 && fb == 0);
-  for (int i = c.tid; i < wcc * Nmax; i += NT) {
-    const int w = i / Nmax, n = i - w * Nmax;
-    const float2 p = reinterpret_cast<const float2*>(c.sPos)[i];
-    c.sNrm[w * np + n] = n < c.nact ? sqrtf(fmaf(p.x, p.x, p.y * p.y)) : 0.f;
-  }
-  if (fb == 0) {
-    // weight-derived matrices of the frame head (see frame_head), once:
-    // K1 = [Wv16 @ Wii | Wv[:,16] | Wv[:,17] | 1 | 0], Wig = Wi @ g, bvg = bv @ g
-    const float* sm = c.sm;
-    const float lam = a.lambda;
-    const int nk1 = kT * kKA, nwig = Nmax * kT;
-    for (int task = c.tid; task < nk1 + nwig + kT; task += NT) {
-      if (task < nk1) {
-        const int t = task / kKA, k = task - t * kKA;
-        float v;
-        if (k < kT) {
-          v = 0.f;
-          for (int d = 0; d < kD; ++d) v = fmaf(sm[SM_WV + t * (kD + 2) + d], sm[SM_WII + d * kT + k], v);
-        } else {
-          v = k == 8 ? sm[SM_WV + t * (kD + 2) + kD] : k == 9 ? sm[SM_WV + t * (kD + 2) + kD + 1]
-                                                      : (k == 10 ? 1.f : 0.f);
-        }
-        c.sm[SM_K1 + task] = v;
-      } else if (task < nk1 + nwig) {
-        const int i = task - nk1, n = i / kT, t2 = i - n * kT;
-        float v = 0.f;
-        for (int d = 0; d < kD; ++d) v = fmaf(c.sWi[n * kD + d], sm[SM_G + d * kT + t2], v);
-        c.sWig[n * kT + t2] = lam * v;
-      } else {
-        const int t2 = task - nk1 - nwig;
-        float v = 0.f;
-        for (int d = 0; d < kD; ++d) v = fmaf(sm[SM_BV + d], sm[SM_G + d * kT + t2], v);
-        c.sm[SM_BVG + t2] = lam * v;
-      }
+  if (c.wv >= kRecW) {
+    const int ntile = (wcc + 3 + 15) / 16;
+    const int ntask = ntile + (fb == 0 ? 1 : 0);
+    for (int task = c.wv - kRecW; task < ntask; task += NP) {
+      if (task < ntile) scene_vtile(a, lay, c, 16 * task, wcc);
+      else scene_kmats(c);
+      SSTAMP(105 + (task & 7), c.lane == 0 && fb == 0);
     }
+  } else {
+    rec_init();
+    SSTAMP(113, c.tid == 0 && fb == 0);
   }
-  mid1();
-  __syncthreads();                                              // B1b: norms, K1, K2, Wig
-  SSTAMP(101, c.tid == 0 && fb == 0);
-  if (fb == 0) {
-    if (c.tid < kD * kT) c.sm[SM_G + c.tid] *= a.lambda;       // ngh = lambda * ngh
-    for (int task = c.tid; task < kL2 * kKA; task += NT) {     // K2 = Wc @ K1
-      const int j = task / kKA, k = task - j * kKA;
-      float v = 0.f;
-      for (int t = 0; t < kT; ++t) v = fmaf(c.sm[SM_WC + j * kT + t], c.sm[SM_K1 + t * kKA + k], v);
-      c.sm[SM_K2 + task] = v;
-    }
-  }
-  // V = norms @ Wi (train.py:179) and VG = norms @ Wig for the chunk's window
-  // rows and the two vislet rows (Ve)
-  for (int task = c.tid; task < (wcc + 2) * (kD + kT); task += NT) {
-    const int w0 = task / (kD + kT), col = task - w0 * (kD + kT);
-    const int w = w0 < wcc ? w0 : lay.wcmax + (w0 - wcc);
-    const float* nr = c.sNrm + w * np;
-    const float* src = col < kD ? c.sWi + col : c.sWig + (col - kD);
-    const int ld = col < kD ? kD : kT;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-    int n = 0;
-    for (; n + 4 <= c.nact; n += 4) {
-      acc0 = fmaf(nr[n], src[n * ld], acc0);
-      acc1 = fmaf(nr[n + 1], src[(n + 1) * ld], acc1);
-      acc2 = fmaf(nr[n + 2], src[(n + 2) * ld], acc2);
-      acc3 = fmaf(nr[n + 3], src[(n + 3) * ld], acc3);
-    }
-    for (; n < c.nact; ++n) acc0 = fmaf(nr[n], src[n * ld], acc0);
-    const float v = (acc0 + acc1) + (acc2 + acc3);
-    if (col < kD) c.sV[w * kD + col] = v;
-    else c.sVG[w * kT + col - kD] = v;
-  }
-  mid2();
-  __syncthreads();                                              // B2: V, Ve
+  __syncthreads();                                              // B2: V, VG, K1, K2
   SSTAMP(2, c.tid == 0 && fb == 0);
+  SSTAMP(101, c.tid == 0 && fb == 0);
 }
 
 // Role 1: the recurrence (waves 0..3).
@@ -1354,25 +1438,28 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   int* seq = reinterpret_cast<int*>(c.sRed + 2 * kRB);   // 2 partial buffers, seq words, row max
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
-    if (fb > 0) scene_pos_dma<NT>(a, c, fb, cnt);
-    scene_stage<NT, TPW * 4>(
-        a, lay, c, fb, cnt,
-        [&] { if (fb == 0) rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L); },
-        [&] {
-          if (fb == 0) {
-            rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
-            asm volatile("" ::: "memory");
-            if (c.lane == 0) seq[c.wv] = 1;
-          }
-        });
+    if (fb > 0) scene_pos_dma<NT>(a, lay, c, fb, cnt);
+    scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, [&] {
+      if (fb == 0) {
+        // softmax(h) numerators: row max exchange (seq 1), then e and its
+        // row partials into buffer 0 (seq 2), no workgroup barrier
+        rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
+        asm volatile("" ::: "memory");
+        if (c.lane == 0) *reinterpret_cast<volatile int*>(seq + c.wv) = 1;
+        poll_seq(seq + (c.L & 3), 1);
+        rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
+        asm volatile("" ::: "memory");
+        if (c.lane == 0) *reinterpret_cast<volatile int*>(seq + c.wv) = 2;
+      }
+    });
     __builtin_amdgcn_s_setprio(2);
     for (int fl = 0; fl < cnt; ++fl) {
       const int g = fb + fl;                 // global frame index
       float4 b, z;
-      poll_frame(seq + (c.L & 3), g + 1, c.sFlag + fl, g + 1,
+      poll_frame(seq + (c.L & 3), g + 2, c.sFlag + fl, g + 1,
                  c.sRing + fl * kD * kD + c.L * kD + 4 * c.q,
                  c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, b, z);
-      rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 2, c.wv, c.q, c.L);
+      rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L);
       SSTAMP(40 + ((fb + fl) & 31), c.tid == 0);
     }
     __builtin_amdgcn_s_setprio(0);
@@ -1419,8 +1506,8 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
-    if (fb > 0) scene_pos_dma<NT>(a, c, fb, cnt);
-    scene_stage<NT, 0>(a, lay, c, fb, cnt, [] {}, [] {});
+    if (fb > 0) scene_pos_dma<NT>(a, lay, c, fb, cnt);
+    scene_stage<NT, NP, 0>(a, lay, c, fb, cnt, [] {});
     load_item(fb, cnt, 0, tgA);       // first tiles' targets: in flight during the heads
     load_item(fb, cnt, 1, tgB);
     // Rm = Wr @ Rel, Rel = Ve * Ve (train.py:194-195, g2k_lstm_mcr.py:106):
@@ -1441,7 +1528,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     for (int fl = pw; fl < cnt; fl += NP) {
       const int f = fb + fl;
       const FrameHeadOut hd =
-          frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, c.sRing + fl * kD * kD,
+          frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                      a.A_out ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
                      a.cost_out ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr, L, q);
       if (L < kL && q < 2) {
@@ -1502,19 +1589,19 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.tid = threadIdx.x; c.lane = c.tid & 63; c.wv = wave_id(); c.L = c.lane & 15; c.q = c.lane >> 4;
   const int Nmax = a.d.Nmax, F = a.d.F;
   c.ntiles = (Nmax + 15) >> 4;
-  c.sWi = smem + lay.o_wi; c.sWo = smem + lay.o_wo; c.sNrm = smem + lay.o_nrm; c.sV = smem + lay.o_v;
+  c.sWi = smem + lay.o_wi; c.sWo = smem + lay.o_wo; c.sVis = smem + lay.o_vis; c.sV = smem + lay.o_v;
   c.sm = smem + lay.o_small; c.sMet = smem + lay.o_met; c.sRing = smem + lay.o_ring;
   c.sMring = smem + lay.o_mring; c.sRed = smem + lay.o_red; c.sPos = smem + lay.o_pos;
-  c.sVG = smem + lay.o_vg; c.sWig = smem + lay.o_wig;
+  c.sVG = smem + lay.o_vg;
   c.sY = smem + lay.o_y;
   c.sFlag = reinterpret_cast<int*>(smem + lay.o_flag);
   SSTAMP(0, c.tid == 0);
   if (F > 0) {
     // issued before n_active / n_frames arrive: the first chunk's window for
     // min(F, fc) frames (a scene with fewer frames reads rows it ignores)
-    const int wv = c.wv, lane = c.lane, np = lay.np;
+    const int wv = c.wv, lane = c.lane;
 #if !defined(G2K_DIAG_PROLOGUE) || G2K_DIAG_PROLOGUE != 2
-    scene_pos_dma<NT>(a, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
+    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
 #endif
 #if !defined(G2K_DIAG_PROLOGUE) || G2K_DIAG_PROLOGUE != 3
     // the small segments: one wave each (one pointer per wave keeps the
@@ -1532,8 +1619,8 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
         case 5: src = a.w.bv; dst = c.sm + SM_BV; n = kD; break;
         case 6: src = a.w.Wr; dst = c.sm + SM_WR; n = kT * 2; break;
         case 7: src = a.w.Wc; dst = c.sm + SM_WC; n = kL2 * kT; break;
-        case 8: src = a.vislet + (size_t)c.s * 2 * Nmax; dst = c.sNrm + lay.wcmax * np; n = Nmax; break;
-        default: src = a.vislet + (size_t)c.s * 2 * Nmax + Nmax; dst = c.sNrm + (lay.wcmax + 1) * np; n = Nmax; break;
+        case 8: src = a.vislet + (size_t)c.s * 2 * Nmax; dst = c.sVis; n = Nmax; break;
+        default: src = a.vislet + (size_t)c.s * 2 * Nmax + Nmax; dst = c.sVis + Nmax; n = Nmax; break;
       }
       for (int i = 0; i < n; i += 64)
         if (i + lane < n)

@@ -37,6 +37,7 @@ for k in range(4):
         continue
     r = v[k] - t0
     print(f"== WG {blk} n_active={b.n_active[blk]}: start {r[0]} dma-issued {r[103]} nf-known {r[104]} vmcnt {r[102]} B1 {r[1]} B1b {r[101]} B2 {r[2]} end {r[100]}")
+    print("   staging tasks done:", " ".join(str(x) for x in r[105:109]), " rec init done:", r[113], " vtile0 entry/loop-end:", r[114], r[115])
     print("   producer flags:", " ".join(str(x) for x in r[3:3 + F]))
     print("   recur done    :", " ".join(str(x) for x in r[40:40 + F]))
     print("   recur per-frame:", " ".join(str(x) for x in np.diff(r[40:40 + F])))
