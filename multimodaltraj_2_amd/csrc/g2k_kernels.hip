@@ -67,22 +67,41 @@ __device__ unsigned long long g2k_stamps[64];
 #endif
 
 #ifdef G2K_STAMPS_SCENE
-// diagnostic build only: timeline of scene-kernel workgroups 0, 85, 170, 255
-__device__ unsigned long long g2k_sstamps[4][128];
+// diagnostic build only: timeline of scene-kernel workgroups 0, 85, 170, 255.
+// Stamps are s_memtime (shader clock, low 32 bits) kept in LDS and copied
+// out at the end, so they do not perturb the vmcnt accounting of the code
+// around them (each still waits lgkmcnt(0) for its own value).
+__device__ unsigned g2k_sstamps[4][128];
+__shared__ unsigned g2k_lds_stamps[128];
 #define SSTAMP(k, cond)                                                         \
   do {                                                                          \
-    if ((cond) && (blockIdx.x % 85) == 0 && blockIdx.x < 340) {                 \
+    if (cond) {                                                                 \
       unsigned long long _t;                                                    \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory"); \
-      g2k_sstamps[blockIdx.x / 85][(k)] = _t;                                   \
+      g2k_lds_stamps[(k)] = (unsigned)_t;                                       \
     }                                                                           \
+  } while (0)
+#define SSTAMP_FLUSH()                                                          \
+  do {                                                                          \
+    __syncthreads();                                                            \
+    if ((blockIdx.x % 85) == 0 && blockIdx.x < 340 && threadIdx.x < 128)       \
+      g2k_sstamps[blockIdx.x / 85][threadIdx.x] = g2k_lds_stamps[threadIdx.x];  \
+  } while (0)
+#define SSTAMP_INIT()                                                           \
+  do {                                                                          \
+    if (threadIdx.x < 128) g2k_lds_stamps[threadIdx.x] = 0xFFFFFFFFu;           \
   } while (0)
 #else
 #define SSTAMP(k, cond) do {} while (0)
+#define SSTAMP_FLUSH() do {} while (0)
+#define SSTAMP_INIT() do {} while (0)
 #endif
 
 
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
 
 // The wave's index in its workgroup, provably wave-uniform (an SGPR): role
 // branches, per-wave loops and s_setprio guards on it compile to scalar
@@ -278,39 +297,68 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
+// Flag / sequence-word store: a plain ds_write_b32 (a volatile store through a
+// generic pointer compiles to a flat store + vmcnt(0) wait, hundreds of cycles
+// on the critical path).  Ordered after the caller's earlier LDS writes by the
+// in-order LDS queue; the memory clobber keeps the compiler from sinking them.
+__device__ __forceinline__ void lds_store_flag(int* p, int v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
 
 
-// One frame's inputs of the recurrence in one LDS round trip.  Lane (L, q)
-// reads ONE recurrence wave's row-partial quad (wave w = L & 3, rows
-// 4q..4q+3) and that wave's sequence word (seq[w] = frames whose partials w
-// has published, +1), the producer's flag of this frame's As tile and the As
-// row quad; the four waves' quads are then summed across each lane quad by
-// DPP.  Each writer stores its data before its word and the words are read
-// before the data, so every lane seeing seq >= want_seq and flag == want_flag
-// means all data read is current.  Busy poll for the first rounds (the
-// scene's critical path), then s_sleep.
-__device__ __forceinline__ void poll_frame(const int* seq_w, int want_seq, const int* flag,
-                                           int want_flag, const float* asrc, const float* rslot,
-                                           float4& b, float4& z) {
-  const uint32_t sa = lds_addr(seq_w), fa = lds_addr(flag), da = lds_addr(asrc), ra = lds_addr(rslot);
-  int sq, fl;
-  f32x4 v, r;
+
+// The recurrence's per-frame exchange, split in two LDS round trips so that
+// the one on the critical path is small:
+//  - read_as: the producer's flag of a frame's As tile, then the lane's As
+//    row quad (As[L][4q..4q+3]), one asm block (LDS serves a CU's requests in
+//    order and the producer stores the tile before the flag, so a current
+//    flag means a current quad).  Issued right after the previous frame's
+//    publish, while the other waves are still finishing theirs.
+//  - poll_red: spin on ONE wave's sequence word (lane L reads wave L & 3's:
+//    seq[w] = frames whose partials w has published, +1) together with that
+//    wave's row-partial quad of rows 4q..4q+3; the four waves' quads are then
+//    summed across each lane quad by DPP.  Data is stored before the word and
+//    read after it, so a current word means current data.
+// Busy poll for the first rounds, then s_sleep.
+__device__ __forceinline__ int read_as(const int* flag, const float* asrc, float4& b) {
+  const uint32_t fa = lds_addr(flag), da = lds_addr(asrc);
+  int fl;
+  f32x4 v;
+  asm volatile(
+      "ds_read_b32 %0, %2\n\t"
+      "ds_read_b128 %1, %3\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(fl), "=&v"(v)
+      : "v"(fa), "v"(da)
+      : "memory");
+  b = make_float4(v[0], v[1], v[2], v[3]);
+  return __builtin_amdgcn_readfirstlane(fl);
+}
+
+// Slow path of read_as: the tile was not ready when first read.
+__device__ __forceinline__ void wait_as(const int* flag, int want, const float* asrc, float4& b) {
   for (int it = 0; it < kPollMax; ++it) {
-    asm volatile(
-        "ds_read_b32 %0, %4\n\t"
-        "ds_read_b32 %1, %5\n\t"
-        "ds_read_b128 %2, %6\n\t"
-        "ds_read_b128 %3, %7\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(sq), "=&v"(fl), "=&v"(v), "=&v"(r)
-        : "v"(sa), "v"(fa), "v"(da), "v"(ra)
-        : "memory");
-    if (__builtin_amdgcn_ballot_w64(sq < want_seq) == 0 &&
-        __builtin_amdgcn_readfirstlane(fl) == want_flag)
-      break;
+    if (read_as(flag, asrc, b) == want) break;
     if (it >= 8) __builtin_amdgcn_s_sleep(1);   // long waits (the first heads): back off
   }
-  b = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ void poll_red(const int* seq_w, int want_seq, const float* rslot,
+                                         float4& z) {
+  const uint32_t sa = lds_addr(seq_w), ra = lds_addr(rslot);
+  int sq;
+  f32x4 r;
+  for (int it = 0; it < kPollMax; ++it) {
+    asm volatile(
+        "ds_read_b32 %0, %2\n\t"
+        "ds_read_b128 %1, %3\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(sq), "=&v"(r)
+        : "v"(sa), "v"(ra)
+        : "memory");
+    if (__builtin_amdgcn_ballot_w64(sq < want_seq) == 0) break;
+    if (it >= 8) __builtin_amdgcn_s_sleep(1);
+  }
   float zz[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -320,6 +368,17 @@ __device__ __forceinline__ void poll_frame(const int* seq_w, int want_seq, const
     zz[i] = t;
   }
   z = make_float4(zz[0], zz[1], zz[2], zz[3]);
+}
+
+// Wait until all four recurrence waves' sequence words reach `want`.
+__device__ __forceinline__ void poll_seq_all(const int* seq, int want) {
+  const uint32_t sa = lds_addr(seq);
+  i32x4 sq;
+  for (int it = 0; it < kPollMax; ++it) {
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(sq) : "v"(sa) : "memory");
+    const int mn = min(min(sq[0], sq[1]), min(sq[2], sq[3]));
+    if (__builtin_amdgcn_readfirstlane(mn) >= want) break;
+  }
 }
 
 // Wait until every lane's sequence word (lane L reads seq_w = seq + (L & 3))
@@ -389,15 +448,17 @@ struct Recur {
                                         const float* red) const {
     float adj[4] = {1.f, 1.f, 1.f, 1.f};
     if (red) {
+      // after a step x holds h' * log2(e) (see body): adj carries the ln 2
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float z = 0.f;
 #pragma unroll
         for (int w = 0; w < NW; ++w) z += red[16 * w + 4 * q + i];
         const float rz = rcp(z);
-        adj[i] = 0.f;
+        float a = 0.f;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) adj[i] = fmaf(red[16 * w + 4 * q + i], rz, adj[i]);
+        for (int w = 0; w < NW; ++w) a = fmaf(red[16 * w + 4 * q + i], rz, a);
+        adj[i] = a * kLn2;
       }
     }
 #pragma unroll
@@ -455,20 +516,35 @@ struct Recur {
       const float4 v = *reinterpret_cast<const float4*>(red_cur + w * 16 + 4 * q);
       z.x += v.x; z.y += v.y; z.z += v.z; z.w += v.w;
     }
-    body(b, z, red_nxt, wv, q, L);
+    body(make_float4(b.x * kLog2e, b.y * kLog2e, b.z * kLog2e, b.w * kLog2e), z, red_nxt, wv, q, L);
     __syncthreads();
   }
 
   // One frame without a workgroup barrier (fused scene kernel): z was polled
   // from the previous exchange (seq words, see poll_frame); after publishing
   // its row partials into red_nxt this wave raises its sequence word.
+  // pf_flag / pf_as: the next frame's As flag and row quad, loaded (flag
+  // first, volatile keeps the order; see read_as) before this frame's MFMAs
+  // so that their LDS latency hides under the MFMA chain.
   __device__ __forceinline__ void step_seq(const float4 b, const float4 z, float* red_nxt,
-                                           int* seq, int seq_val, int wv, int q, int L) {
+                                           int* seq, int seq_val, int wv, int q, int L,
+                                           const int* pf_flag, const float* pf_as, int& pf_fl,
+                                           float4& pf_b) {
+    typedef __attribute__((address_space(3))) volatile int lds_vi;
+    typedef __attribute__((address_space(3))) volatile f32x4 lds_v4;
+    const int fl = *(lds_vi*)(uintptr_t)lds_addr(pf_flag);
+    const f32x4 v = *(lds_v4*)(uintptr_t)lds_addr(pf_as);
     body(b, z, red_nxt, wv, q, L);
     asm volatile("" ::: "memory");   // partials land before the sequence word (LDS is in order)
-    if ((threadIdx.x & 63) == 0) *reinterpret_cast<volatile int*>(seq + wv) = seq_val;
+    if ((threadIdx.x & 63) == 0) lds_store_flag(seq + wv, seq_val);
+    pf_fl = __builtin_amdgcn_readfirstlane(fl);
+    pf_b = make_float4(v[0], v[1], v[2], v[3]);
   }
 
+  // The A operand carries log2(e) (b = As * log2(e), scaled by whoever
+  // stages As): the MFMA yields h' * log2(e) and the next numerators are exp2
+  // of it directly (one v_exp_f32, no scaling multiply on the frame's
+  // critical path); store() takes the ln 2 back.
   __device__ __forceinline__ void body(const float4 b, const float4 z, float* red_nxt, int wv,
                                        int q, int L) {
     const float a0 = b.x * rcp(z.x);
@@ -495,7 +571,7 @@ struct Recur {
       for (int i = 0; i < 4; ++i) {
         const float v = acc[t][i];
         x[t][i] = v;
-        e[t][i] = __expf(v);    // h' in [0, 1]: no max shift needed
+        e[t][i] = __builtin_amdgcn_exp2f(v);    // h' in [0, 1]: no max shift needed
         p[i] += e[t][i];
       }
     publish(red_nxt, p, wv, q, L);
@@ -1086,10 +1162,11 @@ __device__ __forceinline__ void attn_weights(const f32x4 aA, float* as_dst, int 
       R[i] = __expf(aA[i] - mr) * rcp(sr);
     }
   }
+  // stored as As * log2(e): the recurrence's A operand (Recur::body)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float ex = __expf(R[i]);
-    as_dst[(4 * q + i) * kD + L] = ex * rcp(row16_sum(ex));
+    as_dst[(4 * q + i) * kD + L] = ex * (rcp(row16_sum(ex)) * kLog2e);
   }
 }
 
@@ -1242,6 +1319,7 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
 struct SceneCtx {
   float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sY, *sPos, *sVG;
   int* sFlag;
+  int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
   int s, tid, lane, wv, L, q, nact, nf, ntiles;
 };
 
@@ -1445,39 +1523,49 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
         // row partials into buffer 0 (seq 2), no workgroup barrier
         rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
         asm volatile("" ::: "memory");
-        if (c.lane == 0) *reinterpret_cast<volatile int*>(seq + c.wv) = 1;
+        if (c.lane == 0) lds_store_flag(seq + c.wv, 1);
         poll_seq(seq + (c.L & 3), 1);
         rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
         asm volatile("" ::: "memory");
-        if (c.lane == 0) *reinterpret_cast<volatile int*>(seq + c.wv) = 2;
+        if (c.lane == 0) lds_store_flag(seq + c.wv, 2);
       }
     });
     __builtin_amdgcn_s_setprio(2);
+    const float* as_lane = c.sRing + c.L * kD + 4 * c.q;   // this lane's As row quad, frame 0 of the ring
+    float4 b;
+    int flq = read_as(c.sFlag, as_lane, b);
     for (int fl = 0; fl < cnt; ++fl) {
       const int g = fb + fl;                 // global frame index
-      float4 b, z;
-      poll_frame(seq + (c.L & 3), g + 2, c.sFlag + fl, g + 1,
-                 c.sRing + fl * kD * kD + c.L * kD + 4 * c.q,
-                 c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, b, z);
-      rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L);
+      float4 z;
+#ifndef G2K_DIAG_FEW_STAMPS
+      SSTAMP(116 + c.wv, c.lane == 0 && g == 10);
+#endif
+      if (flq != g + 1) wait_as(c.sFlag + fl, g + 1, as_lane + fl * kD * kD, b);
+      poll_red(seq + (c.L & 3), g + 2, c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, z);
+#ifndef G2K_DIAG_FEW_STAMPS
+      SSTAMP(120 + c.wv, c.lane == 0 && g == 10);
+#endif
+      const int fn = fl + 1 < cnt ? fl + 1 : fl;   // next frame's ring slot (itself at the end)
+      rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,
+                  as_lane + fn * kD * kD, flq, b);
+#ifndef G2K_DIAG_FEW_STAMPS
+      SSTAMP(124 + c.wv, c.lane == 0 && g == 10);
       SSTAMP(40 + ((fb + fl) & 31), c.tid == 0);
+#else
+      SSTAMP(40 + ((fb + fl) & 31), c.tid == 0 && (g == 0 || g == 10 || g + 1 == c.nf));
+#endif
     }
     __builtin_amdgcn_s_setprio(0);
     SSTAMP(80 + (c.wv & 15), c.lane == 0);
-    __syncthreads();                                            // B3: chunk done
+    if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
   }
-  __syncthreads();                                              // B4: metric partials
-  if (c.tid < 8) {
-    float v = 0.f;
-    if (c.tid < 5) {
-      if (c.nf > 0)
-        for (int p = 0; p < NP; ++p) v += c.sMet[p * 8 + c.tid];
-    } else if (c.tid == 5) {
-      v = (float)c.nf;
-    }
-    a.metrics[(size_t)c.s * 8 + c.tid] = v;
-  }
+  // epilogue straight off the last frame: wait for every wave's last
+  // partials (its sequence word), h = adj * h', store; no workgroup barrier
+  // (the producers finish the metrics on their own, scene_producer)
+  if (c.nf > 0) poll_seq_all(seq, c.nf + 2);
+  SSTAMP(95, c.tid == 0);
   rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L, c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);
+  SSTAMP(97, c.tid == 0);
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
@@ -1537,7 +1625,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
         *reinterpret_cast<float4*>(m + (kL + L) * kT + 4 * q) = make_float4(hd.mT1[0], hd.mT1[1], hd.mT1[2], hd.mT1[3]);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) *reinterpret_cast<volatile int*>(c.sFlag + fl) = f + 1;
+      if (lane == 0) lds_store_flag(c.sFlag + fl, f + 1);
       SSTAMP(3 + (f & 31), lane == 0);
       __builtin_amdgcn_s_setprio(0);
     }
@@ -1564,19 +1652,37 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       }
     }
     SSTAMP(80 + (c.wv & 15), lane == 0);
-    __syncthreads();                                            // B3: chunk done
+    if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
   }
   if (pw == NP - 1) {
     // frames beyond n_frames: zero predictions (off the critical path)
     for (int i = lane; i < (F - c.nf) * kL2 * Nmax; i += 64)
       a.pred[((size_t)s * F + c.nf) * kL2 * Nmax + i] = 0.f;
   }
+  // metrics: each producer publishes its partial sums, then takes a ticket
+  // (LDS atomic); the wave drawing the last ticket sums the NP rows in
+  // producer order (deterministic) and writes the scene's metrics row
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     const float v = wave_sum(acc[k]);
     if (lane == 0) c.sMet[pw * 8 + k] = v;
   }
-  __syncthreads();                                              // B4
+  int ticket = 0;
+  if (lane == 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // partials before the ticket
+    ticket = atomicAdd(c.sTicket, 1);
+  }
+  ticket = __builtin_amdgcn_readfirstlane(ticket);
+  if (ticket == NP - 1 && lane < 8) {
+    float v = 0.f;
+    if (lane < 5) {
+      if (c.nf > 0)
+        for (int p = 0; p < NP; ++p) v += c.sMet[p * 8 + lane];
+    } else if (lane == 5) {
+      v = (float)c.nf;
+    }
+    a.metrics[(size_t)s * 8 + lane] = v;
+  }
 }
 
 template <int TPW, int NP>
@@ -1595,13 +1701,24 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.sVG = smem + lay.o_vg;
   c.sY = smem + lay.o_y;
   c.sFlag = reinterpret_cast<int*>(smem + lay.o_flag);
+  c.sTicket = reinterpret_cast<int*>(c.sRed + 2 * kRB) + kRecW;
+  SSTAMP_INIT();
+#ifdef G2K_DIAG_TWICE
+  // diagnostic build only: the whole scene twice in one launch (stamps of
+  // the second pass overwrite the first: warm instruction cache / TLB)
+  for (int pass = 0; pass < 2; ++pass) {
+  __syncthreads();
+#endif
   SSTAMP(0, c.tid == 0);
+  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket
   if (F > 0) {
     // issued before n_active / n_frames arrive: the first chunk's window for
     // min(F, fc) frames (a scene with fewer frames reads rows it ignores)
     const int wv = c.wv, lane = c.lane;
 #if !defined(G2K_DIAG_PROLOGUE) || G2K_DIAG_PROLOGUE != 2
+    SSTAMP(92, c.tid == 0 && F > 0);
     scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
+    SSTAMP(93, c.tid == 0);
 #endif
 #if !defined(G2K_DIAG_PROLOGUE) || G2K_DIAG_PROLOGUE != 3
     // the small segments: one wave each (one pointer per wave keeps the
@@ -1628,7 +1745,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
                                            (__attribute__((address_space(3))) void*)(dst + i), 4, 0, 0);
     }
 #endif
-    if (c.tid < kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;   // sequence words
+    SSTAMP(94, c.tid == 0);
     if (c.tid < lay.fc) c.sFlag[c.tid] = 0;              // flags hold (global frame + 1)
   }
   SSTAMP(103, c.tid == 0);
@@ -1642,12 +1759,17 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.nact = clampi(a.n_active[c.s], 0, Nmax);
   c.nf = a.n_frames ? clampi(a.n_frames[c.s], 0, F) : F;
   SSTAMP(104, c.tid == 0 && c.nf >= 0);
+  if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
   if (c.wv < kRecW)
     scene_recurrence<TPW, NP>(a, lay, c);
   else
     scene_producer<NP>(a, lay, c);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
   SSTAMP(100, c.tid == 0);
+#ifdef G2K_DIAG_TWICE
+  }
+#endif
+  SSTAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------
@@ -1979,8 +2101,8 @@ int g2k_abi_version(void) { return G2K_ABI_VERSION; }
 const char* g2k_last_error(void) { return g_err; }
 
 #ifdef G2K_STAMPS_SCENE
-int g2k_debug_sstamps(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2k_sstamps), 4 * 128 * sizeof(unsigned long long));
+int g2k_debug_sstamps(unsigned* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2k_sstamps), 4 * 128 * sizeof(unsigned));
 }
 #endif
 #ifdef G2K_STAMPS
