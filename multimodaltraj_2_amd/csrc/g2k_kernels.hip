@@ -516,37 +516,46 @@ struct Recur {
       const float4 v = *reinterpret_cast<const float4*>(red_cur + w * 16 + 4 * q);
       z.x += v.x; z.y += v.y; z.z += v.z; z.w += v.w;
     }
-    body(make_float4(b.x * kLog2e, b.y * kLog2e, b.z * kLog2e, b.w * kLog2e), z, red_nxt, wv, q, L);
+    int dfl = 0;
+    f32x4 dv = {0.f, 0.f, 0.f, 0.f};
+    body<false>(make_float4(b.x * kLog2e, b.y * kLog2e, b.z * kLog2e, b.w * kLog2e), z, red_nxt, wv, q,
+                L, dfl, dv);
     __syncthreads();
   }
 
   // One frame without a workgroup barrier (fused scene kernel): z was polled
-  // from the previous exchange (seq words, see poll_frame); after publishing
-  // its row partials into red_nxt this wave raises its sequence word.
-  // pf_flag / pf_as: the next frame's As flag and row quad, loaded (flag
-  // first, volatile keeps the order; see read_as) before this frame's MFMAs
-  // so that their LDS latency hides under the MFMA chain.
+  // from the previous exchange (poll_red); after publishing its row partials
+  // into red_nxt this wave raises its sequence word.  pf_flag / pf_as: the
+  // next frame's As flag and row quad (read_as order: flag, then data),
+  // issued before this frame's MFMA chain and waited for after it, so their
+  // LDS latency hides under the chain.  The loads are inline asm without
+  // their own wait; their registers are tied into the waiting asm block
+  // ("+v"), which keeps the compiler from touching them in between.
   __device__ __forceinline__ void step_seq(const float4 b, const float4 z, float* red_nxt,
                                            int* seq, int seq_val, int wv, int q, int L,
                                            const int* pf_flag, const float* pf_as, int& pf_fl,
                                            float4& pf_b) {
-    typedef __attribute__((address_space(3))) volatile int lds_vi;
-    typedef __attribute__((address_space(3))) volatile f32x4 lds_v4;
-    const int fl = *(lds_vi*)(uintptr_t)lds_addr(pf_flag);
-    const f32x4 v = *(lds_v4*)(uintptr_t)lds_addr(pf_as);
-    body(b, z, red_nxt, wv, q, L);
+    int fl;
+    f32x4 v;
+    asm volatile("ds_read_b32 %0, %2\n\tds_read_b128 %1, %3"
+                 : "=&v"(fl), "=&v"(v)
+                 : "v"(lds_addr(pf_flag)), "v"(lds_addr(pf_as))
+                 : "memory");
+    body<true>(b, z, red_nxt, wv, q, L, fl, v);
     asm volatile("" ::: "memory");   // partials land before the sequence word (LDS is in order)
     if ((threadIdx.x & 63) == 0) lds_store_flag(seq + wv, seq_val);
-    pf_fl = __builtin_amdgcn_readfirstlane(fl);
+    pf_fl = fl;   // checked by the caller after its next poll
     pf_b = make_float4(v[0], v[1], v[2], v[3]);
   }
 
   // The A operand carries log2(e) (b = As * log2(e), scaled by whoever
   // stages As): the MFMA yields h' * log2(e) and the next numerators are exp2
   // of it directly (one v_exp_f32, no scaling multiply on the frame's
-  // critical path); store() takes the ln 2 back.
+  // critical path); store() takes the ln 2 back.  PF: wait for step_seq's
+  // prefetch (pf_fl, pf_v) right after the MFMA chain is issued.
+  template <bool PF = false>
   __device__ __forceinline__ void body(const float4 b, const float4 z, float* red_nxt, int wv,
-                                       int q, int L) {
+                                       int q, int L, int& pf_fl, f32x4& pf_v) {
     const float a0 = b.x * rcp(z.x);
     const float a1 = b.y * rcp(z.y);
     const float a2 = b.z * rcp(z.z);
@@ -564,6 +573,7 @@ struct Recur {
 #pragma unroll
     for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a3, e[t][3], acc[t], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
+    if (PF) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pf_fl), "+v"(pf_v)::"memory");
     float p[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
@@ -656,6 +666,7 @@ struct StepArgs {
   float* ws_part;      // [S, nchunk, 8] ADE/FDE partial sums
   float lambda;
   int nchunk;
+  int dma16;           // scene kernel: every input 16-B aligned and Nmax even (16-byte LDS-DMA)
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -1347,6 +1358,60 @@ __device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneLayo
   }
 }
 
+// The scene's inputs by 16-byte LDS-DMA, in few full-width instructions
+// (every LDS-DMA instruction costs the CU's vector-memory path about the
+// same whatever its width, so the prologue issues ~18 of them instead of
+// ~65 narrow ones).  Instruction k of the workgroup (wave k % waves) covers
+// 64 consecutive 16-B slots of one segment; the LDS image of each segment is
+// contiguous in slot order, so the LDS destination is the instruction's
+// base + 16 * lane as LDS-DMA requires.  Segment 0 is the position window
+// with rows padded to R + 1 slots (R = Nmax / 2; the pad slot re-reads the
+// row's first slot); with `weights` the weight / per-scene blocks follow.
+// Requires StepArgs::dma16 (checked on the host).
+template <int NT>
+__device__ __forceinline__ void scene_dma16(const StepArgs& a, const SceneLayout& lay,
+                                            const SceneCtx& c, int fb, int cnt, bool weights) {
+  const int Nmax = a.d.Nmax, R = Nmax >> 1, stride = a.d.stride;
+  const int wcc = (cnt - 1) * stride + kT;
+  const int npos = wcc * (R + 1);
+  const int ipos = (npos + 63) >> 6;
+  const float* psrc = a.pos + ((size_t)c.s * a.d.W + (size_t)fb * stride) * Nmax * 2;
+  constexpr int kSeg = 9;
+  const float* src[kSeg] = {a.w.Wi, a.w.Wo, a.w.Wii, a.w.Wv, a.w.bv, a.w.Wr, a.w.Wc,
+                            a.G + (size_t)c.s * kD * kT, a.vislet + (size_t)c.s * 2 * Nmax};
+  float* dst[kSeg] = {c.sWi, c.sWo, c.sm + SM_WII, c.sm + SM_WV, c.sm + SM_BV, c.sm + SM_WR,
+                      c.sm + SM_WC, c.sm + SM_G, c.sVis};
+  const int n16[kSeg] = {4 * Nmax, 2 * Nmax, kD * kT / 4, kT * (kD + 2) / 4, kD / 4, kT * 2 / 4,
+                         kL2 * kT / 4, kD * kT / 4, R};
+  int ninst = ipos;
+  if (weights) {
+#pragma unroll
+    for (int i = 0; i < kSeg; ++i) ninst += (n16[i] + 63) >> 6;
+  }
+  for (int k = c.wv; k < ninst; k += NT / 64) {
+    if (k < ipos) {
+      const int t = 64 * k + c.lane;
+      if (t < npos) {
+        const int row = t / (R + 1);
+        int col = t - row * (R + 1);
+        col = col == R ? 0 : col;
+        dma16(psrc + (size_t)row * 2 * Nmax + 4 * col, c.sPos + 256 * k);
+      }
+    } else {
+      int j = k - ipos;
+#pragma unroll
+      for (int i = 0; i < kSeg; ++i) {
+        const int ni = (n16[i] + 63) >> 6;
+        if (j >= 0 && j < ni) {
+          const int t = 64 * j + c.lane;
+          if (t < n16[i]) dma16(src[i] + 4 * t, dst[i] + 256 * j);
+        }
+        j -= ni;
+      }
+    }
+  }
+}
+
 // One 16-row tile of the chunk's embedding rows, by MFMA (train.py:76-79,
 // 167-195): local rows r = w0 + L are the window rows (r < wcc: norms
 // ||pos||, formed here from the LDS window), the two vislet rows and a bv
@@ -1516,7 +1581,10 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   int* seq = reinterpret_cast<int*>(c.sRed + 2 * kRB);   // 2 partial buffers, seq words, row max
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
-    if (fb > 0) scene_pos_dma<NT>(a, lay, c, fb, cnt);
+    if (fb > 0) {
+      if (a.dma16) scene_dma16<NT>(a, lay, c, fb, cnt, false);
+      else scene_pos_dma<NT>(a, lay, c, fb, cnt);
+    }
     scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, [&] {
       if (fb == 0) {
         // softmax(h) numerators: row max exchange (seq 1), then e and its
@@ -1532,29 +1600,61 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     });
     __builtin_amdgcn_s_setprio(2);
     const float* as_lane = c.sRing + c.L * kD + 4 * c.q;   // this lane's As row quad, frame 0 of the ring
-    float4 b;
-    int flq = read_as(c.sFlag, as_lane, b);
-    for (int fl = 0; fl < cnt; ++fl) {
+    // one frame; (b, flq): this frame's prefetched As quad and flag, (bn,
+    // fln): where the next frame's prefetch goes.  Unrolled by two with the
+    // pairs swapped so that a prefetch never needs a register copy (a copy
+    // at the loop edge waits for every outstanding LDS op, the publish too).
+    auto frame = [&](int fl, float4& b, int& flq, float4& bn, int& fln) {
       const int g = fb + fl;                 // global frame index
       float4 z;
 #ifndef G2K_DIAG_FEW_STAMPS
       SSTAMP(116 + c.wv, c.lane == 0 && g == 10);
 #endif
-      if (flq != g + 1) wait_as(c.sFlag + fl, g + 1, as_lane + fl * kD * kD, b);
       poll_red(seq + (c.L & 3), g + 2, c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, z);
+      if (__builtin_amdgcn_readfirstlane(flq) != g + 1) wait_as(c.sFlag + fl, g + 1, as_lane + fl * kD * kD, b);
 #ifndef G2K_DIAG_FEW_STAMPS
       SSTAMP(120 + c.wv, c.lane == 0 && g == 10);
 #endif
       const int fn = fl + 1 < cnt ? fl + 1 : fl;   // next frame's ring slot (itself at the end)
       rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,
-                  as_lane + fn * kD * kD, flq, b);
+                  as_lane + fn * kD * kD, fln, bn);
 #ifndef G2K_DIAG_FEW_STAMPS
       SSTAMP(124 + c.wv, c.lane == 0 && g == 10);
       SSTAMP(40 + ((fb + fl) & 31), c.tid == 0);
 #else
       SSTAMP(40 + ((fb + fl) & 31), c.tid == 0 && (g == 0 || g == 10 || g + 1 == c.nf));
 #endif
+    };
+    float4 b0, b1;
+    int f0 = read_as(c.sFlag, as_lane, b0), f1 = 0;
+    for (int fl = 0; fl < cnt; fl += 2) {
+      frame(fl, b0, f0, b1, f1);
+      if (fl + 1 < cnt) frame(fl + 1, b1, f1, b0, f0);
     }
+#ifdef G2K_DIAG_RECUR_REPEAT
+    // diagnostic build only: 1000 more recurrence frames on frame 0's As
+    // after the real ones (the producers are done by then): the steady-state
+    // cost of one frame inside this kernel, stamps 72 / 73
+    if (fb + lay.fc >= c.nf) {
+      SSTAMP(72, c.tid == 0);
+      float4 ba, bb;
+      int fa = read_as(c.sFlag, as_lane, ba), fbb = 0;
+      int sl = 0;   // ring slot cycling through the chunk's real As tiles
+      for (int it = 0; it < 1000; it += 2) {
+        const int g0 = c.nf + it, g1 = g0 + 1;
+        float4 z;
+        sl = sl + 1 < cnt ? sl + 1 : 0;
+        poll_red(seq + (c.L & 3), g0 + 2, c.sRed + (g0 & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, z);
+        rc.step_seq(ba, z, c.sRed + ((g0 + 1) & 1) * kRB, seq, g0 + 3, c.wv, c.q, c.L, c.sFlag + sl,
+                    as_lane + sl * kD * kD, fbb, bb);
+        sl = sl + 1 < cnt ? sl + 1 : 0;
+        poll_red(seq + (c.L & 3), g1 + 2, c.sRed + (g1 & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, z);
+        rc.step_seq(bb, z, c.sRed + ((g1 + 1) & 1) * kRB, seq, g1 + 3, c.wv, c.q, c.L, c.sFlag + sl,
+                    as_lane + sl * kD * kD, fa, ba);
+      }
+      SSTAMP(73, c.tid == 0);
+    }
+#endif
     __builtin_amdgcn_s_setprio(0);
     SSTAMP(80 + (c.wv & 15), c.lane == 0);
     if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
@@ -1594,7 +1694,10 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
-    if (fb > 0) scene_pos_dma<NT>(a, lay, c, fb, cnt);
+    if (fb > 0) {
+      if (a.dma16) scene_dma16<NT>(a, lay, c, fb, cnt, false);
+      else scene_pos_dma<NT>(a, lay, c, fb, cnt);
+    }
     scene_stage<NT, NP, 0>(a, lay, c, fb, cnt, [] {});
     load_item(fb, cnt, 0, tgA);       // first tiles' targets: in flight during the heads
     load_item(fb, cnt, 1, tgB);
@@ -1710,17 +1813,30 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   __syncthreads();
 #endif
   SSTAMP(0, c.tid == 0);
+#ifdef G2K_STAMPS_SCENE
+  if (c.lane == 0) {   // placement: HW_ID (SIMD_ID bits 5:4, CU_ID 11:8, SE_ID 15:13)
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    g2k_lds_stamps[60 + c.wv] = hw;
+  }
+  if (c.tid == 0) {
+    unsigned long long rt;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt)::"memory");
+    g2k_lds_stamps[98] = (unsigned)rt;
+  }
+#endif
   if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket
   if (F > 0) {
     // issued before n_active / n_frames arrive: the first chunk's window for
     // min(F, fc) frames (a scene with fewer frames reads rows it ignores)
     const int wv = c.wv, lane = c.lane;
-#if !defined(G2K_DIAG_PROLOGUE) || G2K_DIAG_PROLOGUE != 2
     SSTAMP(92, c.tid == 0 && F > 0);
+    if (a.dma16) {
+      scene_dma16<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc, true);
+      SSTAMP(93, c.tid == 0);
+    } else {
     scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
     SSTAMP(93, c.tid == 0);
-#endif
-#if !defined(G2K_DIAG_PROLOGUE) || G2K_DIAG_PROLOGUE != 3
     // the small segments: one wave each (one pointer per wave keeps the
     // kernel-argument loads off a serial s_load / s_waitcnt chain)
     for (int seg = wv; seg < 10; seg += NT / 64) {
@@ -1744,7 +1860,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i + lane),
                                            (__attribute__((address_space(3))) void*)(dst + i), 4, 0, 0);
     }
-#endif
+    }
     SSTAMP(94, c.tid == 0);
     if (c.tid < lay.fc) c.sFlag[c.tid] = 0;              // flags hold (global frame + 1)
   }
@@ -1766,6 +1882,13 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     scene_producer<NP>(a, lay, c);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
   SSTAMP(100, c.tid == 0);
+#ifdef G2K_STAMPS_SCENE
+  if (c.tid == 0) {   // wall clock (100 MHz) beside the shader-clock stamps
+    unsigned long long rt;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt)::"memory");
+    g2k_lds_stamps[99] = (unsigned)rt;
+  }
+#endif
 #ifdef G2K_DIAG_TWICE
   }
 #endif
@@ -2054,7 +2177,11 @@ bool use_split_step() {
 
 template <int NP>
 int launch_scene_np(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
-  const size_t lds = (size_t)l.total * 4;
+  size_t lds = (size_t)l.total * 4;
+  if (const char* e = getenv("G2K_LDS_MIN_KB")) {   // tuning: occupancy experiments
+    const size_t m = (size_t)atoi(e) * 1024;
+    if (m > lds && m <= 160 * 1024) lds = m;
+  }
   const dim3 g(a.d.S), b(64 * (kRecW + NP));
   switch (a.d.H / 64) {
     case 1: hipLaunchKernelGGL((g2k_scene_kernel<1, NP>), g, b, lds, st, a, l); break;
@@ -2153,6 +2280,10 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
   a.n_active = n_active; a.n_frames = n_frames; a.ped_mask = ped_mask; a.h_in = h_in;
   a.h_out = h_out; a.pred = pred; a.metrics = metrics; a.A_out = A_out; a.cost_out = cost_out;
   a.lambda = lambda; a.nchunk = p.nchunk;
+  a.dma16 = (d->Nmax % 2 == 0) && aligned16(pos) && aligned16(vislet) && aligned16(G) &&
+            aligned16(w->Wi) && aligned16(w->Wo) && aligned16(w->Wii) && aligned16(w->Wv) &&
+            aligned16(w->bv) && aligned16(w->Wr) && aligned16(w->Wc);
+  if (const char* e = getenv("G2K_NO_DMA16")) if (atoi(e) == 1) a.dma16 = 0;   // A/B switch
   a.ws_as = static_cast<float*>(workspace);
   a.ws_part = a.ws_as + (size_t)d->S * d->F * kD * kD;
   hipStream_t st = (hipStream_t)stream;

@@ -46,3 +46,9 @@ for k in range(4):
     print("   frame10 poll-start w0..3:", " ".join(str(x) for x in r[116:120]))
     print("   frame10 poll-done  w0..3:", " ".join(str(x) for x in r[120:124]))
     print("   frame10 published  w0..3:", " ".join(str(x) for x in r[124:128]))
+    rt = (raw[k, 99] - raw[k, 98]) % (1 << 32)
+    print(f"   realtime start->end: {rt} ticks of 10 ns = {rt * 10} ns; shader-clock ticks {r[100]} -> {r[100] / max(rt * 10, 1):.3f} GHz")
+    hw = raw[k, 60:72]
+    print("   wave SIMD ids:", " ".join(str((int(h) >> 4) & 3) for h in hw), " CU", (int(hw[0]) >> 8) & 15, "SE", (int(hw[0]) >> 13) & 7)
+    if raw[k, 73] != 0xFFFFFFFF:
+        print(f"   repeat loop: {(int(raw[k, 73]) - int(raw[k, 72])) % (1 << 32) / 1000:.1f} cycles/frame")

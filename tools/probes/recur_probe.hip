@@ -45,6 +45,8 @@ __device__ __forceinline__ uint32_t dup_pk(float x) {
   return *reinterpret_cast<uint32_t*>(&v);
 }
 
+constexpr int kNB = 256, kIters = 2000;
+
 template <int EX, int FL, int TPW, int NW>
 __global__ void __launch_bounds__(64 * NW) probe(const float* __restrict__ as_g, float* out,
                                                  unsigned long long* cyc, int iters) {
@@ -61,6 +63,7 @@ __global__ void __launch_bounds__(64 * NW) probe(const float* __restrict__ as_g,
   for (int t = 0; t < TPW; ++t)
     for (int i = 0; i < 4; ++i) { e[t][i] = 1.0f + 0.01f * (L + t + i + q); x[t][i] = 0.f; }
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
   for (int g = 0; g < iters; ++g) {
     float4 b = *reinterpret_cast<const float4*>(sAs + L * 16 + 4 * q);
     float z[4];
@@ -178,14 +181,15 @@ __global__ void __launch_bounds__(64 * NW) probe(const float* __restrict__ as_g,
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
   if (lane == 0) cyc[blockIdx.x * NW + wv] = t1 - t0;
+  if (tid == 0 && blockIdx.x == 0) cyc[kNB * 16 - 1] = (t1 - t0) * 1000 / ((r1 - r0) * 10);
   float sacc = 0.f;
   for (int t = 0; t < TPW; ++t)
     for (int i = 0; i < 4; ++i) sacc += x[t][i];
   out[blockIdx.x * 64 * NW + tid] = sacc;
 }
 
-constexpr int kNB = 256, kIters = 2000;
 
 template <int EX, int FL, int TPW, int NW>
 void run(const char* name, const float* as, float* out, unsigned long long* cyc) {
@@ -195,9 +199,11 @@ void run(const char* name, const float* as, float* out, unsigned long long* cyc)
   }
   std::vector<unsigned long long> c(kNB * NW);
   (void)hipMemcpy(c.data(), cyc, c.size() * 8, hipMemcpyDeviceToHost);
+  unsigned long long mhz;
+  (void)hipMemcpy(&mhz, cyc + kNB * 16 - 1, 8, hipMemcpyDeviceToHost);
   std::sort(c.begin(), c.end());
-  printf("%-40s cycles/frame: min %7.1f median %7.1f max %7.1f\n", name, c[0] / (double)kIters,
-         c[c.size() / 2] / (double)kIters, c.back() / (double)kIters);
+  printf("%-40s cycles/frame: min %7.1f median %7.1f max %7.1f  (clock %llu MHz)\n", name, c[0] / (double)kIters,
+         c[c.size() / 2] / (double)kIters, c.back() / (double)kIters, mhz);
 }
 
 int main() {
