@@ -282,9 +282,6 @@ __device__ __forceinline__ void attn_row_pass(float* A, int r, float* gout) {
 // yields wrong numbers, not a hung GPU.
 // ---------------------------------------------------------------------------
 constexpr int kPollMax = 1 << 20;
-#ifndef G2K_DIAG_TILE
-#define G2K_DIAG_TILE 0   // diagnostic builds only: 1 no errors, 2 no pred stores, 4 no MFMA
-#endif
 #ifndef G2K_POLL_SLEEP
 #define G2K_POLL_SLEEP 1
 #endif
@@ -1071,7 +1068,7 @@ constexpr int kKA = 12;        // augmented contraction length (8 window rows + 
 
 struct SceneLayout {
   int fc, wcmax, pp;   // frames per chunk, window rows per chunk, pos row pitch (floats)
-  int o_wi, o_wo, o_vis, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_red, o_pos, o_vg;
+  int o_wi, o_wo, o_vis, o_v, o_small, o_met, o_ring, o_mring, o_flag, o_mflag, o_red, o_pos, o_vg;
   int total;   // floats
 };
 
@@ -1086,11 +1083,11 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
-  s.o_y = o;     o += NP * kD * kL2;
   s.o_met = o;   o += NP * 8;
   s.o_ring = o;  o += fc * kD * kD;
   s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
-  s.o_flag = o;  o += rup4(fc);
+  s.o_flag = o;  o += rup4(fc);                      // As ring flags (recurrence polls)
+  s.o_mflag = o; o += rup4(fc);                      // M ring flags (prediction tiles poll)
   s.o_red = o;   o += 4 * 16 * kRecW;
   s.o_pos = o;   o += s.wcmax * s.pp;                  // raw position window (LDS-DMA)
   s.o_vg = o;    o += rup4((s.wcmax + 3) * kT);       // VG = V @ g: window, Ve0, Ve1, bv rows
@@ -1191,11 +1188,13 @@ __device__ __forceinline__ void attn_weights(const f32x4 aA, float* as_dst, int 
 //   M    = Wc @ cost = K2 @ VGaug                                   (:119)
 // Contractions over the 12 augmented rows use k = 4 ks + q (3 k-steps);
 // A contracts over t = 4q + ks (rows of E as the MFMA left them).
-// As goes to `as_dst`; the x / y row tiles of M^T are returned (M[L][4q+i]).
+// As goes to `as_dst` (do_as); the x / y row tiles of M^T are returned
+// (M[L][4q+i]).
 __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float* sV,
                                                    const float* sVG, int wrow0, int wcmax,
                                                    const float (&rm)[4], float lam, float* as_dst,
-                                                   float* A_g, float* cost_g, int L, int q) {
+                                                   float* A_g, float* cost_g, int L, int q,
+                                                   bool do_as) {
   float ka[3], ua[3], va[3];
 #pragma unroll
   for (int ks = 0; ks < 3; ++ks) {
@@ -1223,14 +1222,16 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
     o.mT0 = mfma4(va[ks], bx, o.mT0);   // M[L][4q+i]       (x rows)
     o.mT1 = mfma4(va[ks], by, o.mT1);   // M[12+L][4q+i]    (y rows)
   }
-  float em[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) em[i] = eN[i] * rm[i];                      // rm = 0 for t >= 8
   f32x4 aA = {0.f, 0.f, 0.f, 0.f};
+  if (do_as || A_g) {
+    float em[4];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const float gA = q < 2 ? lam * sm[SM_G + L * kT + 4 * q + ks] : 0.f;  // g[r = L][t]
-    aA = mfma4(gA, em[ks], aA);                                          // A[4q+i][L]
+    for (int i = 0; i < 4; ++i) em[i] = eN[i] * rm[i];                    // rm = 0 for t >= 8
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const float gA = q < 2 ? lam * sm[SM_G + L * kT + 4 * q + ks] : 0.f;  // g[r = L][t]
+      aA = mfma4(gA, em[ks], aA);                                        // A[4q+i][L]
+    }
   }
   if (A_g) {
 #pragma unroll
@@ -1245,69 +1246,62 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
       for (int i = 0; i < 4; ++i) cost_g[(4 * q + i) * kT + L] = cC[i];
     }
   }
-  attn_weights(aA, as_dst, L, q);
+  if (do_as) attn_weights(aA, as_dst, L, q);
   return o;
 }
 
-// One 16-pedestrian tile of one frame: Y^T = Wo^T @ M^T (M = this frame's
-// [24][8] from the M ring), pred stores, a9 error terms (4 lanes per
-// pedestrian) accumulated into acc.  The contraction over t (8) uses
-// k = 4 ks + q, so two k-steps cover it without zero padding.
-__device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys,
-                                          float* pr, const float2 (&tg)[3], const uint8_t* pm,
-                                          int Nmax, int nact, int t, int L, int q, int lane,
-                                          float acc[5]) {
+// One 16-pedestrian tile of one frame on the VALU (the matrix pipe is left
+// to the recurrence waves, which share the SIMDs): Y[r][n] = sum_t M[r][t]
+// Wo[t][n] (models/g2k_lstm_mcr.py:122; M = the frame's [24][8] from the M
+// ring).  Lane (pp = lane >> 2, u = lane & 3) owns pedestrian n = 16 t + pp
+// and prediction steps 3u .. 3u + 2 (x and y rows): it stores them and forms
+// the a9 error terms of its steps; the four lanes of a pedestrian are summed
+// by DPP quad exchanges.
+__device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* pr,
+                                          const float2 (&tg)[3], const uint8_t* pm, int Nmax,
+                                          int nact, int t, int lane, float acc[5]) {
   const int pp = lane >> 2, u = lane & 3;
-  const int n0 = 16 * t;
-  const int ne = n0 + pp;
-  const bool has_t = ne < nact && (pm ? pm[ne] != 0 : true);
-  f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
+  const int n = 16 * t + pp;
+  const int nc = n < Nmax ? n : Nmax - 1;
+  const bool live = n < nact;
+  const bool has_t = live && (pm ? pm[nc] != 0 : true);
+  float wo[kT];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int n = n0 + L, k = 4 * ks + q;
-    const float wo = n < nact ? sWo[k * Nmax + n] : 0.f;
-    const float bx = L < kL ? M[L * kT + k] : 0.f;
-    const float by = L < kL ? M[(kL + L) * kT + k] : 0.f;
-#if (G2K_DIAG_TILE & 4)
-    y0[ks] = wo * bx; y1[ks] = wo * by;   // diagnostic build only
-#else
-    y0 = mfma4(wo, bx, y0);   // Y[L][n0 + 4q + i]
-    y1 = mfma4(wo, by, y1);   // Y[12 + L][n0 + 4q + i]
-#endif
+  for (int k = 0; k < kT; ++k) wo[k] = live ? sWo[k * Nmax + nc] : 0.f;
+  float yx[3], yy[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float4* mx = reinterpret_cast<const float4*>(M + (3 * u + j) * kT);
+    const float4* my = reinterpret_cast<const float4*>(M + (kL + 3 * u + j) * kT);
+    const float4 x0 = mx[0], x1 = mx[1], y0 = my[0], y1 = my[1];
+    float sx = x0.x * wo[0], sy = y0.x * wo[0];
+    sx = fmaf(x0.y, wo[1], sx); sy = fmaf(y0.y, wo[1], sy);
+    sx = fmaf(x0.z, wo[2], sx); sy = fmaf(y0.z, wo[2], sy);
+    sx = fmaf(x0.w, wo[3], sx); sy = fmaf(y0.w, wo[3], sy);
+    sx = fmaf(x1.x, wo[4], sx); sy = fmaf(y1.x, wo[4], sy);
+    sx = fmaf(x1.y, wo[5], sx); sy = fmaf(y1.y, wo[5], sy);
+    sx = fmaf(x1.z, wo[6], sx); sy = fmaf(y1.z, wo[6], sy);
+    sx = fmaf(x1.w, wo[7], sx); sy = fmaf(y1.w, wo[7], sy);
+    yx[j] = sx;
+    yy[j] = sy;
   }
-  if (L < kL) {
-    const int nb = n0 + 4 * q;
-#if !(G2K_DIAG_TILE & 2)
-    if (nb + 3 < Nmax && ((Nmax & 3) == 0)) {
-      *reinterpret_cast<float4*>(pr + L * Nmax + nb) = make_float4(y0[0], y0[1], y0[2], y0[3]);
-      *reinterpret_cast<float4*>(pr + (kL + L) * Nmax + nb) = make_float4(y1[0], y1[1], y1[2], y1[3]);
-    } else {
+  if (n < Nmax) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (nb + i < Nmax) { pr[L * Nmax + nb + i] = y0[i]; pr[(kL + L) * Nmax + nb + i] = y1[i]; }
+    for (int j = 0; j < 3; ++j) {
+      pr[(3 * u + j) * Nmax + n] = yx[j];
+      pr[(kL + 3 * u + j) * Nmax + n] = yy[j];
     }
-#endif
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<float2*>(ys + (4 * q + i) * kL2 + 2 * L) = make_float2(y0[i], y1[i]);
   }
-#if (G2K_DIAG_TILE & 1)
-  return;   // diagnostic build only
-#endif
-  __builtin_amdgcn_wave_barrier();
   float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f, fx = 0.f, fy = 0.f;
-  const float2* yp = reinterpret_cast<const float2*>(ys + pp * kL2) + 3 * u;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float2 yv = yp[k];
-    const float dx = yv.x - tg[k].x, dy = yv.y - tg[k].y;
+    const float dx = yx[k] - tg[k].x, dy = yy[k] - tg[k].y;
     ea = fmaf(dx, dx, ea);
     eb = fmaf(dx, dy, eb);
     ec = fmaf(dy, dy, ec);
     el2 += __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
     fx = dx; fy = dy;
   }
-  __builtin_amdgcn_wave_barrier();
   ea += dpp<0xB1>(ea); ea += dpp<0x4E>(ea);
   eb += dpp<0xB1>(eb); eb += dpp<0x4E>(eb);
   ec += dpp<0xB1>(ec); ec += dpp<0x4E>(ec);
@@ -1328,8 +1322,9 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
 
 // Per-workgroup context of the scene kernel (LDS carve-up, scene scalars).
 struct SceneCtx {
-  float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sY, *sPos, *sVG;
-  int* sFlag;
+  float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sPos, *sVG;
+  int* sFlag;     // As ring: global frame + 1 once the frame's As is in its slot
+  int* sMflag;    // M ring: global frame + 1 once the frame's M is in its slot
   int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
   int s, tid, lane, wv, L, q, nact, nf, ntiles;
 };
@@ -1534,11 +1529,103 @@ __device__ __forceinline__ void scene_kmats(const SceneCtx& c) {
   }
 }
 
+// The first kRecW frame heads of a chunk on the recurrence waves (wave w:
+// chunk frame w), between the staging barriers: they read only the LDS
+// window and the weights (not the staging tiles' V / VG or K1 / K2), so they
+// run beside the producers' staging and As_0 is in the ring when the
+// recurrence starts instead of one producer head later.  Only As
+// (train.py:240) is formed here; these frames' M and optional A / cost
+// outputs stay with the producers (frame_head with do_as = false).
+// v_mfma_f32_16x16x4_f32 chain (lane (L, q), register i = row 4q + i):
+//   K1^T = Wii^T @ Wv[:, :16]^T        K1[t = L][4q + i]: the A operand of E
+//   Vaug = Naug @ Wi                   rows 0..7 the frame's window norms
+//                                      (train.py:76-85), 8, 9 the vislet rows
+//                                      (Ve, train.py:182-183)
+//   E    = [K1 | Wv16 | Wv17] @ Vaug + bv              (g2k_lstm_mcr.py:105)
+//   A    = (lambda G) @ (E * Rm),  Rm = Wr @ (Ve * Ve)  (:105-106)
+__device__ __forceinline__ void scene_rec_head(const StepArgs& a, const SceneLayout& lay,
+                                               const SceneCtx& c, int fb, int fl) {
+  const int Nmax = a.d.Nmax, L = c.L, q = c.q, L7 = L & 7, nact = c.nact;
+  const float* sm = c.sm;
+  float aw[4], bw[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int d = 4 * q + ks;
+    aw[ks] = L < kT ? sm[SM_WII + d * kT + L7] : 0.f;          // Wii[d][m = L]
+    bw[ks] = L < kT ? sm[SM_WV + L7 * (kD + 2) + d] : 0.f;     // Wv[t = L][d]
+  }
+  f32x4 k1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) k1 = mfma4(aw[ks], bw[ks], k1);   // K1[L][4q + i]
+  // Vaug: A operand Naug[r = L][n], B operand Wi[n][d = L], n = 4 ks + q
+  const bool win = L < kT, vis = L == kT || L == kT + 1;
+  const float* prow = c.sPos + (fl * a.d.stride + L7) * lay.pp;
+  const float* vrow = c.sVis + (L == kT + 1 ? Nmax : 0);
+  auto nload = [&](int ks, float& wi, float2& p, float& v) {
+    const int n = 4 * ks + q;
+    const int nc = n < Nmax ? n : Nmax - 1;
+    wi = c.sWi[nc * kD + L];
+    p = *reinterpret_cast<const float2*>(prow + 2 * nc);
+    v = vrow[nc];
+  };
+  auto nval = [&](int ks, const float2 p, float v) {
+    const int n = 4 * ks + q;
+    const float nrm = __builtin_amdgcn_sqrtf(fmaf(p.x, p.x, p.y * p.y));
+    return n < nact ? (win ? nrm : (vis ? v : 0.f)) : 0.f;
+  };
+  const int nks = (Nmax + 3) / 4;
+  f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+  int ks = 0;
+  for (; ks + 2 <= nks; ks += 2) {
+    float w0, w1, u0, u1;
+    float2 p0, p1;
+    nload(ks, w0, p0, u0);
+    nload(ks + 1, w1, p1, u1);
+    v0 = mfma4(nval(ks, p0, u0), w0, v0);
+    v1 = mfma4(nval(ks + 1, p1, u1), w1, v1);
+  }
+  if (ks < nks) {
+    float w0, u0;
+    float2 p0;
+    nload(ks, w0, p0, u0);
+    v0 = mfma4(nval(ks, p0, u0), w0, v0);
+  }
+  f32x4 vt;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) vt[i] = v0[i] + v1[i];            // Vaug[4q + i][L]
+  f32x4 eN = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float ak = q < 2 ? k1[k] : ((q == 2 && k < 2) ? sm[SM_WV + L7 * (kD + 2) + kD + k] : 0.f);
+    eN = mfma4(L < kT ? ak : 0.f, vt[k], eN);                    // E[4q + i][L] - bv[L]
+  }
+  // Ve rows live in lane group q = 2 (registers 0, 1): fetch column L's
+  const float ve0 = __int_as_float(__builtin_amdgcn_ds_bpermute((L + 32) << 2, __float_as_int(vt[0])));
+  const float ve1 = __int_as_float(__builtin_amdgcn_ds_bpermute((L + 32) << 2, __float_as_int(vt[1])));
+  const float bvl = sm[SM_BV + L];
+  float em[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = 4 * q + i;
+    const float rm = q < 2 ? fmaf(sm[SM_WR + 2 * t], ve0 * ve0, sm[SM_WR + 2 * t + 1] * (ve1 * ve1)) : 0.f;
+    em[i] = (eN[i] + bvl) * rm;
+  }
+  f32x4 aA = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float gA = q < 2 ? a.lambda * sm[SM_G + L * kT + 4 * q + k] : 0.f;   // g[r = L][t]
+    aA = mfma4(gA, em[k], aA);                                              // A[4q + i][L]
+  }
+  attn_weights(aA, c.sRing + fl * kD * kD, L, q);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (c.lane == 0) lds_store_flag(c.sFlag + fl, fb + fl + 1);
+}
+
 // Chunk staging shared by both roles (every wave takes part).  The chunk's
-// position window is in flight by LDS-DMA (scene_pos_dma).  Wait, barrier;
-// the producer waves compute the embedding-row tiles (scene_vtile) and, at
-// the first chunk, K1 / K2 (scene_kmats) while `rec_init` runs on the
-// recurrence waves; barrier.
+// position window is in flight by LDS-DMA.  Wait, barrier; the producer
+// waves compute the embedding-row tiles (scene_vtile) and, at the first
+// chunk, K1 / K2 (scene_kmats) while `rec_init` runs on the recurrence
+// waves (softmax(h) numerators, the first frame heads); barrier.
 template <int NT, int NP, int VMC, typename RecInit>
 __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int fb, int cnt, RecInit rec_init) {
@@ -1586,12 +1673,17 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
       else scene_pos_dma<NT>(a, lay, c, fb, cnt);
     }
     scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, [&] {
+      // softmax(h) numerators (first chunk): row max exchange (seq 1), then
+      // e and its row partials into buffer 0 (seq 2), no workgroup barrier;
+      // the chunk's first kRecW frame heads in between (scene_rec_head)
       if (fb == 0) {
-        // softmax(h) numerators: row max exchange (seq 1), then e and its
-        // row partials into buffer 0 (seq 2), no workgroup barrier
         rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
         asm volatile("" ::: "memory");
         if (c.lane == 0) lds_store_flag(seq + c.wv, 1);
+      }
+      if (c.wv < cnt) scene_rec_head(a, lay, c, fb, c.wv);
+      SSTAMP(74 + c.wv, c.lane == 0 && fb == 0);
+      if (fb == 0) {
         poll_seq(seq + (c.L & 3), 1);
         rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
         asm volatile("" ::: "memory");
@@ -1675,7 +1767,6 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   constexpr int NT = 64 * (kRecW + NP);
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
   const int pw = c.wv - kRecW, L = c.L, q = c.q, lane = c.lane, s = c.s, ntiles = c.ntiles;
-  float* ys = c.sY + pw * kD * kL2;
   const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
   // tile items of a chunk: item j -> frame j / ntiles, tile j % ntiles;
   // this producer takes items pw, pw + NP, ...  (k-th item: j = pw + k * NP)
@@ -1712,23 +1803,29 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
         rm[i] = q < 2 ? fmaf(c.sm[SM_WR + 2 * t], ve0 * ve0, c.sm[SM_WR + 2 * t + 1] * (ve1 * ve1)) : 0.f;
       }
     }
-    // phase 1 — the critical path: frame heads in frame order, As + M into
-    // the rings, then the frame's flag; the first four frames' heads get the
-    // issue priority (the recurrence starts on them)
-    if (pw < 4) __builtin_amdgcn_s_setprio(1);
+    // phase 1 — the critical path: frame heads in frame order, M (and As
+    // from chunk frame kRecW on: the recurrence waves head the first kRecW)
+    // into the rings, then the frame's flags; the first heads the
+    // recurrence will wait for get the issue priority
     for (int fl = pw; fl < cnt; fl += NP) {
       const int f = fb + fl;
+      const bool do_as = fl >= kRecW;
+      if (do_as && fl < 2 * kRecW) __builtin_amdgcn_s_setprio(1);
       const FrameHeadOut hd =
           frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                      a.A_out ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
-                     a.cost_out ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr, L, q);
+                     a.cost_out ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr, L, q,
+                     do_as);
       if (L < kL && q < 2) {
         float* m = c.sMring + fl * kL2 * kT;
         *reinterpret_cast<float4*>(m + L * kT + 4 * q) = make_float4(hd.mT0[0], hd.mT0[1], hd.mT0[2], hd.mT0[3]);
         *reinterpret_cast<float4*>(m + (kL + L) * kT + 4 * q) = make_float4(hd.mT1[0], hd.mT1[1], hd.mT1[2], hd.mT1[3]);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) lds_store_flag(c.sFlag + fl, f + 1);
+      if (lane == 0) {
+        lds_store_flag(c.sMflag + fl, f + 1);
+        if (do_as) lds_store_flag(c.sFlag + fl, f + 1);
+      }
       SSTAMP(3 + (f & 31), lane == 0);
       __builtin_amdgcn_s_setprio(0);
     }
@@ -1742,9 +1839,9 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       const int j = pw + k * NP;
       const int fl = j / ntiles, t = j - fl * ntiles;
       const int f = fb + fl;
-      poll_flag(c.sFlag + fl, f + 1);          // M of this frame (maybe another producer's)
-      pred_tile(c.sMring + fl * kL2 * kT, c.sWo, ys, a.pred + ((size_t)s * F + f) * kL2 * Nmax, tg, pm, Nmax, c.nact, t,
-                L, q, lane, acc);
+      poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)
+      pred_tile(c.sMring + fl * kL2 * kT, c.sWo, a.pred + ((size_t)s * F + f) * kL2 * Nmax, tg, pm,
+                Nmax, c.nact, t, lane, acc);
     };
     for (int k = 0; k < nitems; k += 2) {
       item(k, tgA);
@@ -1802,8 +1899,8 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.sm = smem + lay.o_small; c.sMet = smem + lay.o_met; c.sRing = smem + lay.o_ring;
   c.sMring = smem + lay.o_mring; c.sRed = smem + lay.o_red; c.sPos = smem + lay.o_pos;
   c.sVG = smem + lay.o_vg;
-  c.sY = smem + lay.o_y;
   c.sFlag = reinterpret_cast<int*>(smem + lay.o_flag);
+  c.sMflag = reinterpret_cast<int*>(smem + lay.o_mflag);
   c.sTicket = reinterpret_cast<int*>(c.sRed + 2 * kRB) + kRecW;
   SSTAMP_INIT();
 #ifdef G2K_DIAG_TWICE
@@ -1862,7 +1959,10 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     }
     }
     SSTAMP(94, c.tid == 0);
-    if (c.tid < lay.fc) c.sFlag[c.tid] = 0;              // flags hold (global frame + 1)
+    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)
+      c.sFlag[c.tid] = 0;
+      c.sMflag[c.tid] = 0;
+    }
   }
   SSTAMP(103, c.tid == 0);
 #ifdef G2K_DIAG_PROLOGUE

@@ -177,3 +177,50 @@ def test_ade_fde_variants(gpu):
         complete = p1[s][:, :n].reshape(2, 12, n).transpose(2, 1, 0)
         ade, fde, cnt = ref.get_mean_error(complete, t1[s][:n], 8, n)
         assert close(out1[s, :3], [ade, fde, cnt]) <= TOL
+
+
+def _check_all(b, out, res, S):
+    pred = out.pred.cpu().numpy()
+    hh = out.h.cpu().numpy()
+    met = out.metrics.cpu().numpy()
+    for s in range(S):
+        n = int(b.n_active[s])
+        pr, h, m, ex = res[s]
+        nf = pr.shape[0]
+        assert close(pred[s, :nf, :, :n].reshape(nf, 2, 12, n), pr) <= TOL
+        assert np.all(pred[s, :, :, n:] == 0)
+        assert close(hh[s], h) <= TOL
+        assert close(met[s, :6], m[:6]) <= TOL
+
+
+@pytest.mark.parametrize("S,Nmax,H,F", [(3, 7, 64, 20), (2, 32, 128, 40), (2, 30, 64, 33)])
+def test_step_fallbacks_and_chunks(gpu, S, Nmax, H, F):
+    """Odd Nmax takes the 4-byte staging path (no 16-B LDS-DMA); F beyond the
+    32-frame chunk exercises the chunked prologue (fb > 0) and the recurrence
+    waves' heads of a later chunk; Nmax = 30 has an odd number of 16-B slots
+    per position row."""
+    b, out, res = run_both(S, Nmax, H, F=F, device=gpu)
+    _check_all(b, out, res, S)
+
+
+@pytest.mark.parametrize("env", ["G2K_NO_DMA16", "G2K_STEP_SPLIT"])
+def test_step_paths_agree(gpu, monkeypatch, env):
+    """The 16-B and the 4-byte LDS-DMA staging move the same bytes, so they
+    must agree bitwise; the two-kernel split sums in another order and is
+    held to the parity tolerance."""
+    b = make_batch(4, 32, 128, seed=9)
+    params = fs.init_params(32, seed=0, device=gpu)
+    t = b.to_device(gpu)
+    args = (params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+    o1 = fs.step_fused(*args)
+    torch.cuda.synchronize()
+    monkeypatch.setenv(env, "1")
+    o2 = fs.step_fused(*args)
+    torch.cuda.synchronize()
+    if env == "G2K_NO_DMA16":
+        assert torch.equal(o1.pred, o2.pred)
+        assert torch.equal(o1.h, o2.h)
+        assert torch.equal(o1.metrics, o2.metrics)
+    else:
+        assert close(o2.pred.cpu().numpy(), o1.pred.cpu().numpy()) <= TOL
+        assert close(o2.h.cpu().numpy(), o1.h.cpu().numpy()) <= TOL

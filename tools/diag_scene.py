@@ -38,6 +38,7 @@ for k in range(4):
     r = np.where(raw[k] == 0xFFFFFFFF, -1, (raw[k] - raw[k, 0]) % (1 << 32))
     print(f"== WG {blk} n_active={b.n_active[blk]}: start {r[0]} dma-issued {r[103]} nf-known {r[104]} vmcnt {r[102]} B1 {r[1]} B2 {r[2]} end {r[100]}")
     print("   prologue: args-ready", r[92], "pos-dma-issued", r[93], "segs-issued", r[94], " epilogue: B3", r[95], "B4", r[96], "h-stored", r[97])
+    print("   rec heads done w0..3:", " ".join(str(x) for x in r[74:78]))
     print("   staging tasks done:", " ".join(str(x) for x in r[105:109]), " rec init done:", r[113], " vtile0 entry/loop-end:", r[114], r[115])
     print("   producer flags:", " ".join(str(x) for x in r[3:3 + F]))
     print("   recur done    :", " ".join(str(x) for x in r[40:40 + F]))
