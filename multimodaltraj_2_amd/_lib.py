@@ -73,7 +73,8 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # G2K_LIB_PATH: A/B tooling only (tools/ab), never set by tests / bench defaults
+    p = path or os.environ.get("G2K_LIB_PATH") or LIB_PATH
     if not os.path.exists(p):
         raise G2KLibraryError(
             f"{p} not found: the HIP library is not built (run `python __graft_entry__.py`); "

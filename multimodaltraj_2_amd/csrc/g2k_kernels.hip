@@ -664,6 +664,7 @@ struct StepArgs {
   float lambda;
   int nchunk;
   int dma16;           // scene kernel: every input 16-B aligned and Nmax even (16-byte LDS-DMA)
+  int opts;            // scene kernel options (kOpt*)
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -1057,6 +1058,18 @@ __global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(RecurArgs a) {
 // workgroup barriers only at chunk boundaries.
 // ---------------------------------------------------------------------------
 constexpr int kSceneChunk = 32;
+// scene kernel options (StepArgs::opts; G2K_SCENE_OPTS overrides the default)
+constexpr int kOptRecHeads = 1;    // the recurrence waves head each chunk's first kRecW frames
+constexpr int kOptValuTiles = 2;   // prediction tiles on the VALU (else MFMA)
+constexpr int kModeDma16 = 4;      // 16-byte LDS-DMA staging (StepArgs::dma16)
+// Defaults off: at eth_hotel_synth the recurrence-wave heads cost +1.3 us per
+// step (they take ~4.5k cycles beside the staging tiles and delay the
+// second barrier) and the VALU tiles +0.2 us (gpurun_out d30).
+constexpr int kSceneOptsDefault = 0;
+// A scene kernel is compiled per MODE (options | kModeDma16) so that each
+// instantiation holds only the code it runs: every workgroup fetches its
+// code cold at launch, and measured step time grows with the kernel's code
+// bytes (~1.2 us per 8 KB at S = 256).
 constexpr int kRecW = 4;
 // scene-kernel small block: the split path's offsets plus weight-derived
 // matrices (DESIGN.md "frame head"): K1 = [Wv16 @ Wii | Wv16.. | Wv17.. | 1 | 0]
@@ -1068,7 +1081,7 @@ constexpr int kKA = 12;        // augmented contraction length (8 window rows + 
 
 struct SceneLayout {
   int fc, wcmax, pp;   // frames per chunk, window rows per chunk, pos row pitch (floats)
-  int o_wi, o_wo, o_vis, o_v, o_small, o_met, o_ring, o_mring, o_flag, o_mflag, o_red, o_pos, o_vg;
+  int o_wi, o_wo, o_vis, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_mflag, o_red, o_pos, o_vg;
   int total;   // floats
 };
 
@@ -1083,6 +1096,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
+  s.o_y = o;     o += NP * kD * kL2;                  // MFMA tiles' transpose scratch
   s.o_met = o;   o += NP * 8;
   s.o_ring = o;  o += fc * kD * kD;
   s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
@@ -1320,9 +1334,77 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
   }
 }
 
+// The same tile by MFMA (scene option kOptValuTiles off): Y^T = Wo^T @ M^T (M = this frame's
+// [24][8] from the M ring), pred stores, a9 error terms (4 lanes per
+// pedestrian) accumulated into acc.  The contraction over t (8) uses
+// k = 4 ks + q, so two k-steps cover it without zero padding.
+__device__ __forceinline__ void pred_tile_mfma(const float* M, const float* sWo, float* ys,
+                                          float* pr, const float2 (&tg)[3], const uint8_t* pm,
+                                          int Nmax, int nact, int t, int L, int q, int lane,
+                                          float acc[5]) {
+  const int pp = lane >> 2, u = lane & 3;
+  const int n0 = 16 * t;
+  const int ne = n0 + pp;
+  const bool has_t = ne < nact && (pm ? pm[ne] != 0 : true);
+  f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int n = n0 + L, k = 4 * ks + q;
+    const float wo = n < nact ? sWo[k * Nmax + n] : 0.f;
+    const float bx = L < kL ? M[L * kT + k] : 0.f;
+    const float by = L < kL ? M[(kL + L) * kT + k] : 0.f;
+    y0 = mfma4(wo, bx, y0);   // Y[L][n0 + 4q + i]
+    y1 = mfma4(wo, by, y1);   // Y[12 + L][n0 + 4q + i]
+  }
+  if (L < kL) {
+    const int nb = n0 + 4 * q;
+    if (nb + 3 < Nmax && ((Nmax & 3) == 0)) {
+      *reinterpret_cast<float4*>(pr + L * Nmax + nb) = make_float4(y0[0], y0[1], y0[2], y0[3]);
+      *reinterpret_cast<float4*>(pr + (kL + L) * Nmax + nb) = make_float4(y1[0], y1[1], y1[2], y1[3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (nb + i < Nmax) { pr[L * Nmax + nb + i] = y0[i]; pr[(kL + L) * Nmax + nb + i] = y1[i]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float2*>(ys + (4 * q + i) * kL2 + 2 * L) = make_float2(y0[i], y1[i]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f, fx = 0.f, fy = 0.f;
+  const float2* yp = reinterpret_cast<const float2*>(ys + pp * kL2) + 3 * u;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float2 yv = yp[k];
+    const float dx = yv.x - tg[k].x, dy = yv.y - tg[k].y;
+    ea = fmaf(dx, dx, ea);
+    eb = fmaf(dx, dy, eb);
+    ec = fmaf(dy, dy, ec);
+    el2 += __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
+    fx = dx; fy = dy;
+  }
+  __builtin_amdgcn_wave_barrier();
+  ea += dpp<0xB1>(ea); ea += dpp<0x4E>(ea);
+  eb += dpp<0xB1>(eb); eb += dpp<0x4E>(eb);
+  ec += dpp<0xB1>(ec); ec += dpp<0x4E>(ec);
+  el2 += dpp<0xB1>(el2); el2 += dpp<0x4E>(el2);
+  fx = dpp<0xFF>(fx);   // quad_perm [3,3,3,3]: the fde vector lives in quarter 3
+  fy = dpp<0xFF>(fy);
+  if (has_t && u == 0) {
+    const float hm = 0.5f * (ea - ec);
+    const float lam = 0.5f * (ea + ec) + __builtin_amdgcn_sqrtf(fmaf(hm, hm, eb * eb));
+    const float fsq = fmaf(fx, fx, fy * fy);
+    acc[0] += __builtin_amdgcn_sqrtf(fmaxf(lam, 0.f)) * (1.0f / 12.0f);
+    acc[1] += 1.0f;
+    acc[2] += fsq;
+    acc[3] += el2 * (1.0f / 12.0f);
+    acc[4] += __builtin_amdgcn_sqrtf(fsq);
+  }
+}
+
 // Per-workgroup context of the scene kernel (LDS carve-up, scene scalars).
 struct SceneCtx {
-  float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sPos, *sVG;
+  float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sPos, *sVG, *sY;
   int* sFlag;     // As ring: global frame + 1 once the frame's As is in its slot
   int* sMflag;    // M ring: global frame + 1 once the frame's M is in its slot
   int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
@@ -1655,7 +1737,7 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
 }
 
 // Role 1: the recurrence (waves 0..3).
-template <int TPW, int NP>
+template <int TPW, int NP, int MODE>
 __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneLayout& lay,
                                                  const SceneCtx& c) {
   constexpr int NT = 64 * (kRecW + NP);
@@ -1669,7 +1751,7 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) {
-      if (a.dma16) scene_dma16<NT>(a, lay, c, fb, cnt, false);
+      if constexpr ((MODE & kModeDma16) != 0) scene_dma16<NT>(a, lay, c, fb, cnt, false);
       else scene_pos_dma<NT>(a, lay, c, fb, cnt);
     }
     scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, [&] {
@@ -1681,7 +1763,9 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
         asm volatile("" ::: "memory");
         if (c.lane == 0) lds_store_flag(seq + c.wv, 1);
       }
-      if (c.wv < cnt) scene_rec_head(a, lay, c, fb, c.wv);
+      if constexpr ((MODE & kOptRecHeads) != 0) {
+        if (c.wv < cnt) scene_rec_head(a, lay, c, fb, c.wv);
+      }
       SSTAMP(74 + c.wv, c.lane == 0 && fb == 0);
       if (fb == 0) {
         poll_seq(seq + (c.L & 3), 1);
@@ -1761,7 +1845,7 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
-template <int NP>
+template <int NP, int MODE>
 __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLayout& lay,
                                                const SceneCtx& c) {
   constexpr int NT = 64 * (kRecW + NP);
@@ -1786,7 +1870,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) {
-      if (a.dma16) scene_dma16<NT>(a, lay, c, fb, cnt, false);
+      if constexpr ((MODE & kModeDma16) != 0) scene_dma16<NT>(a, lay, c, fb, cnt, false);
       else scene_pos_dma<NT>(a, lay, c, fb, cnt);
     }
     scene_stage<NT, NP, 0>(a, lay, c, fb, cnt, [] {});
@@ -1809,8 +1893,9 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // recurrence will wait for get the issue priority
     for (int fl = pw; fl < cnt; fl += NP) {
       const int f = fb + fl;
-      const bool do_as = fl >= kRecW;
-      if (do_as && fl < 2 * kRecW) __builtin_amdgcn_s_setprio(1);
+      constexpr bool kHeads = (MODE & kOptRecHeads) != 0;
+      const bool do_as = !kHeads || fl >= kRecW;
+      if (kHeads ? (do_as && fl < 2 * kRecW) : fl < kRecW) __builtin_amdgcn_s_setprio(1);
       const FrameHeadOut hd =
           frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                      a.A_out ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
@@ -1840,8 +1925,12 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       const int fl = j / ntiles, t = j - fl * ntiles;
       const int f = fb + fl;
       poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)
-      pred_tile(c.sMring + fl * kL2 * kT, c.sWo, a.pred + ((size_t)s * F + f) * kL2 * Nmax, tg, pm,
-                Nmax, c.nact, t, lane, acc);
+      float* pr = a.pred + ((size_t)s * F + f) * kL2 * Nmax;
+      if constexpr ((MODE & kOptValuTiles) != 0)
+        pred_tile(c.sMring + fl * kL2 * kT, c.sWo, pr, tg, pm, Nmax, c.nact, t, lane, acc);
+      else
+        pred_tile_mfma(c.sMring + fl * kL2 * kT, c.sWo, c.sY + pw * kD * kL2, pr, tg, pm, Nmax, c.nact,
+                       t, L, q, lane, acc);
     };
     for (int k = 0; k < nitems; k += 2) {
       item(k, tgA);
@@ -1885,7 +1974,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   }
 }
 
-template <int TPW, int NP>
+template <int TPW, int NP, int MODE>
 __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   constexpr int NT = 64 * (kRecW + NP);
   constexpr int kRB = 16 * kRecW;
@@ -1901,6 +1990,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.sVG = smem + lay.o_vg;
   c.sFlag = reinterpret_cast<int*>(smem + lay.o_flag);
   c.sMflag = reinterpret_cast<int*>(smem + lay.o_mflag);
+  c.sY = smem + lay.o_y;
   c.sTicket = reinterpret_cast<int*>(c.sRed + 2 * kRB) + kRecW;
   SSTAMP_INIT();
 #ifdef G2K_DIAG_TWICE
@@ -1928,7 +2018,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     // min(F, fc) frames (a scene with fewer frames reads rows it ignores)
     const int wv = c.wv, lane = c.lane;
     SSTAMP(92, c.tid == 0 && F > 0);
-    if (a.dma16) {
+    if constexpr ((MODE & kModeDma16) != 0) {
       scene_dma16<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc, true);
       SSTAMP(93, c.tid == 0);
     } else {
@@ -1977,9 +2067,9 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   SSTAMP(104, c.tid == 0 && c.nf >= 0);
   if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
   if (c.wv < kRecW)
-    scene_recurrence<TPW, NP>(a, lay, c);
+    scene_recurrence<TPW, NP, MODE>(a, lay, c);
   else
-    scene_producer<NP>(a, lay, c);
+    scene_producer<NP, MODE>(a, lay, c);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
   SSTAMP(100, c.tid == 0);
 #ifdef G2K_STAMPS_SCENE
@@ -2275,6 +2365,37 @@ bool use_split_step() {
   return env && atoi(env) == 1;
 }
 
+// One scene-kernel launch; MODE = options | kModeDma16 selects the
+// instantiation.  Every (TPW, NP) has the default-option modes; the bench
+// geometry (TPW 2, NP 8) has all option modes for A/B runs.
+template <int TPW, int NP, int MODE>
+void launch_scene_k(const StepArgs& a, const SceneLayout& l, size_t lds, hipStream_t st) {
+  hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, MODE>), dim3(a.d.S), dim3(64 * (kRecW + NP)), lds, st,
+                     a, l);
+}
+
+template <int TPW, int NP>
+int launch_scene_mode(const StepArgs& a, const SceneLayout& l, size_t lds, hipStream_t st) {
+  const int mode = a.opts | (a.dma16 ? kModeDma16 : 0);
+  constexpr int kD0 = kSceneOptsDefault, kD1 = kSceneOptsDefault | kModeDma16;
+  if (mode == kD0) { launch_scene_k<TPW, NP, kD0>(a, l, lds, st); return G2K_OK; }
+  if (mode == kD1) { launch_scene_k<TPW, NP, kD1>(a, l, lds, st); return G2K_OK; }
+  if constexpr (TPW == 2 && NP == 8) {
+    switch (mode) {
+      case 0: launch_scene_k<2, 8, 0>(a, l, lds, st); return G2K_OK;
+      case 1: launch_scene_k<2, 8, 1>(a, l, lds, st); return G2K_OK;
+      case 2: launch_scene_k<2, 8, 2>(a, l, lds, st); return G2K_OK;
+      case 3: launch_scene_k<2, 8, 3>(a, l, lds, st); return G2K_OK;
+      case 4: launch_scene_k<2, 8, 4>(a, l, lds, st); return G2K_OK;
+      case 5: launch_scene_k<2, 8, 5>(a, l, lds, st); return G2K_OK;
+      case 6: launch_scene_k<2, 8, 6>(a, l, lds, st); return G2K_OK;
+      case 7: launch_scene_k<2, 8, 7>(a, l, lds, st); return G2K_OK;
+      default: break;
+    }
+  }
+  return set_err(G2K_EUNSUPPORTED, "scene options %d not built for H=%d, NP=%d", a.opts, a.d.H, NP);
+}
+
 template <int NP>
 int launch_scene_np(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
   size_t lds = (size_t)l.total * 4;
@@ -2282,22 +2403,16 @@ int launch_scene_np(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
     const size_t m = (size_t)atoi(e) * 1024;
     if (m > lds && m <= 160 * 1024) lds = m;
   }
-  const dim3 g(a.d.S), b(64 * (kRecW + NP));
   switch (a.d.H / 64) {
-    case 1: hipLaunchKernelGGL((g2k_scene_kernel<1, NP>), g, b, lds, st, a, l); break;
-    case 2: hipLaunchKernelGGL((g2k_scene_kernel<2, NP>), g, b, lds, st, a, l); break;
-    case 4: hipLaunchKernelGGL((g2k_scene_kernel<4, NP>), g, b, lds, st, a, l); break;
+    case 1: return launch_scene_mode<1, NP>(a, l, lds, st);
+    case 2: return launch_scene_mode<2, NP>(a, l, lds, st);
+    case 4: return launch_scene_mode<4, NP>(a, l, lds, st);
     default: return set_err(G2K_EUNSUPPORTED, "H=%d unsupported with %d producer waves", a.d.H, NP);
   }
-  return G2K_OK;
 }
 
 int launch_scene(const StepArgs& a, const SceneLayout& l, int NP, hipStream_t st) {
-  if (a.d.H == 512) {
-    hipLaunchKernelGGL((g2k_scene_kernel<8, 4>), dim3(a.d.S), dim3(64 * (kRecW + 4)),
-                       (size_t)l.total * 4, st, a, l);
-    return G2K_OK;
-  }
+  if (a.d.H == 512) return launch_scene_mode<8, 4>(a, l, (size_t)l.total * 4, st);
   switch (NP) {
     case 4: return launch_scene_np<4>(a, l, st);
     case 6: return launch_scene_np<6>(a, l, st);
@@ -2383,7 +2498,11 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
   a.dma16 = (d->Nmax % 2 == 0) && aligned16(pos) && aligned16(vislet) && aligned16(G) &&
             aligned16(w->Wi) && aligned16(w->Wo) && aligned16(w->Wii) && aligned16(w->Wv) &&
             aligned16(w->bv) && aligned16(w->Wr) && aligned16(w->Wc);
-  if (const char* e = getenv("G2K_NO_DMA16")) if (atoi(e) == 1) a.dma16 = 0;   // A/B switch
+  // 16-byte staging measured 0.6 us per step SLOWER than the 4-byte LDS-DMA
+  // at eth_hotel_synth (gpurun_out d30: 20.3 vs 19.6 us), so it is opt-in
+  if (const char* e = getenv("G2K_DMA16")) { if (atoi(e) != 1) a.dma16 = 0; } else a.dma16 = 0;
+  a.opts = kSceneOptsDefault;
+  if (const char* e = getenv("G2K_SCENE_OPTS")) a.opts = atoi(e) & 3;          // A/B switch
   a.ws_as = static_cast<float*>(workspace);
   a.ws_part = a.ws_as + (size_t)d->S * d->F * kD * kD;
   hipStream_t st = (hipStream_t)stream;

@@ -195,7 +195,8 @@ def _check_all(b, out, res, S):
 
 @pytest.mark.parametrize("S,Nmax,H,F", [(3, 7, 64, 20), (2, 32, 128, 40), (2, 30, 64, 33)])
 def test_step_fallbacks_and_chunks(gpu, S, Nmax, H, F):
-    """Odd Nmax takes the 4-byte staging path (no 16-B LDS-DMA); F beyond the
+    """Odd Nmax and Nmax = 30 (odd 16-B slots per row) under the default
+    4-byte staging; F beyond the
     32-frame chunk exercises the chunked prologue (fb > 0) and the recurrence
     waves' heads of a later chunk; Nmax = 30 has an odd number of 16-B slots
     per position row."""
@@ -203,21 +204,24 @@ def test_step_fallbacks_and_chunks(gpu, S, Nmax, H, F):
     _check_all(b, out, res, S)
 
 
-@pytest.mark.parametrize("env", ["G2K_NO_DMA16", "G2K_STEP_SPLIT"])
-def test_step_paths_agree(gpu, monkeypatch, env):
+@pytest.mark.parametrize("env,val", [("G2K_DMA16", "1"), ("G2K_STEP_SPLIT", "1"),
+                                     ("G2K_SCENE_OPTS", "1"), ("G2K_SCENE_OPTS", "2"),
+                                     ("G2K_SCENE_OPTS", "3")])
+def test_step_paths_agree(gpu, monkeypatch, env, val):
     """The 16-B and the 4-byte LDS-DMA staging move the same bytes, so they
-    must agree bitwise; the two-kernel split sums in another order and is
-    held to the parity tolerance."""
+    must agree bitwise; the two-kernel split and the scene-kernel options
+    (recurrence-wave heads, VALU prediction tiles) sum in another order and
+    are held to the parity tolerance."""
     b = make_batch(4, 32, 128, seed=9)
     params = fs.init_params(32, seed=0, device=gpu)
     t = b.to_device(gpu)
     args = (params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
     o1 = fs.step_fused(*args)
     torch.cuda.synchronize()
-    monkeypatch.setenv(env, "1")
+    monkeypatch.setenv(env, val)
     o2 = fs.step_fused(*args)
     torch.cuda.synchronize()
-    if env == "G2K_NO_DMA16":
+    if env == "G2K_DMA16":
         assert torch.equal(o1.pred, o2.pred)
         assert torch.equal(o1.h, o2.h)
         assert torch.equal(o1.metrics, o2.metrics)
