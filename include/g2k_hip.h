@@ -85,9 +85,10 @@ int64_t g2k_step_workspace_bytes(const g2k_dims* d);
  *   a9 validation ADE/FDE sums (train.py:640-674).
  * Replaces: the frame loop train.py:197-276 (four sess.run + ~13 .eval() per
  * frame) and its per-batch setup train.py:178-195.
- * Two stream-ordered launches: a frame-parallel kernel (a2-a7, a9) and the
- * frame-sequential recurrence kernel (a8); `workspace` carries the attention
- * weights between them (g2k_step_workspace_bytes).
+ * One launch of the wave-specialised scene kernel (one workgroup per scene:
+ * producer waves run a2-a7 / a9 per frame, recurrence waves run a8, LDS flags
+ * between them).  G2K_STEP_SPLIT=1 selects the older two-launch split
+ * (frame-parallel kernel + recurrence kernel, As handed over in `workspace`).
  *
  *   pos      [S, W, Nmax, 2]       pedestrian (x, y) rows
  *   vislet   [S, 2, Nmax]          load_traj.py:139 rows 4:6 slice
@@ -164,6 +165,61 @@ int g2k_infer_rlns_f32(const float* adj, float* out, int64_t rows, int32_t cols,
                        void* stream);
 int g2k_eval_rln_ngh_f32(const float* adj, float* out, int64_t rows,
                          int32_t cols, void* stream);
+
+/*
+ * g2k_gridlstm_f32 — one step of the GridLSTMCell neighbourhood encoders (a6):
+ * tf.contrib.rnn.GridLSTMCell(num_units, feature_size, frequency_skip =
+ * feature_size, share_time_frequency_weights=True,
+ * couple_input_forget_gates=True, state_is_tuple=False), peepholes optional;
+ * dataflow decoded from the reference's saved graph.
+ * Replaces: helper.py:31-39 + 68 (neighborhood_vis_loc_encoder.forward, with
+ * peepholes) and helper.py:131-141 (neighborhood_stat_enc, no peepholes).
+ *   in        [rows, ld_in]     frequency block k = columns k*fs .. k*fs+fs-1
+ *   state     [rows, ld_state]  block k: c_time = columns 2u*k .. 2u*k+u-1,
+ *                               m_time = the next u columns
+ *   W [fs + 2u, 3u] (W_f_0_0), b [3u] (B_f_0),
+ *   peep [4, u] = (wIf, wIt, wOf, wOt) (W_{I,O}_diag_freq{f,t}_0) or NULL
+ *   out       [rows, blocks*2u] = concat_k [m_time', m_freq']
+ *   state_out [rows, blocks*2u] = concat_k [c_time', m_time']
+ *             (may alias state only when ld_state == blocks*2u)
+ * Built for num_units in {1, 2, 4} and feature_size in {2, 4, 8}.
+ */
+int g2k_gridlstm_f32(const float* in, int64_t ld_in, const float* state, int64_t ld_state,
+                     const float* W, const float* b, const float* peep, float* out,
+                     float* state_out, int64_t rows, int32_t blocks, int32_t feature_size,
+                     int32_t num_units, void* stream);
+
+/*
+ * Train mode (SURVEY.md §8(d) "--mode train", §8(e) gradient all-reduce).  The
+ * reference has no loss or optimizer for this model (SURVEY.md finding 5);
+ * these entry points are the build's.  loss = 1/2 the summed squared error of
+ * pred_path_band against `targets` over frames < n_frames and the active,
+ * masked pedestrians (the pairs the a9 errors use).
+ *
+ * g2k_grad_size: floats P in one parameter vector = 24*Nmax + 496, laid out
+ *   in g2k_weights order (Wi, Wii, Wv, bv, Wr, Wc, Wo; padded shapes); -1 on
+ *   invalid dims.
+ * g2k_grad_workspace_bytes: device workspace g2k_step_grad_f32 needs.
+ * g2k_step_grad_f32: grad [P + 2] = {d loss / d params summed over the S
+ *   scenes (P floats), loss, count of (frame, pedestrian) pairs}, fixed
+ *   reduction order (deterministic).  Inputs as g2k_step_fused_f32.  Wr's
+ *   gradient is exactly zero (the attention does not reach the predictions).
+ * g2k_update_f32: params [P] -= the optimizer step for
+ *   g = grad[:P] / max(grad[P+1], 1), clipped by global norm when
+ *   grad_clip > 0 (g * clip / max(||g||, clip)), then RMSProp when ms [P] is
+ *   given (ms = decay*ms + (1-decay) g^2; p -= lr g / sqrt(ms + 1e-10)) or SGD
+ *   (ms NULL).  argParser.py:38-47: grad_clip 10, learning_rate 0.005,
+ *   decay_rate 0.95.  Across ranks, all-reduce the [P + 2] grad first.
+ */
+int64_t g2k_grad_size(const g2k_dims* d);
+int64_t g2k_grad_workspace_bytes(const g2k_dims* d);
+int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
+                      const float* vislet, const float* G, const float* targets,
+                      const int32_t* n_active, const int32_t* n_frames,
+                      const uint8_t* ped_mask, float lambda, float* grad, void* workspace,
+                      int64_t workspace_bytes, void* stream);
+int g2k_update_f32(float* params, float* ms, const float* grad, int64_t n_params, float lr,
+                   float decay, float grad_clip, void* stream);
 
 #ifdef __cplusplus
 }

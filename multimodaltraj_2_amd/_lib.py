@@ -45,6 +45,14 @@ SYMBOLS = {
                                 c_vp, c_vp]),
     "g2k_infer_rlns_f32": (c_int, [c_vp, c_vp, c_i64, c_i32, c_vp]),
     "g2k_eval_rln_ngh_f32": (c_int, [c_vp, c_vp, c_i64, c_i32, c_vp]),
+    "g2k_gridlstm_f32": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                 c_i32, c_i32, c_i32, c_vp]),
+    "g2k_grad_size": (c_i64, [ctypes.POINTER(G2KDims)]),
+    "g2k_grad_workspace_bytes": (c_i64, [ctypes.POINTER(G2KDims)]),
+    "g2k_step_grad_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
+                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp,
+                                  c_i64, c_vp]),
+    "g2k_update_f32": (c_int, [c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_vp]),
 }
 
 ABI_VERSION = 1

@@ -2270,6 +2270,439 @@ __global__ void __launch_bounds__(64) g2k_row_softmax_kernel(const float* __rest
 }
 
 // ---------------------------------------------------------------------------
+// a6 GridLSTMCell (helper.py:31-39 vis/loc encoder, 131-141 static encoder):
+// tf.contrib.rnn GridLSTMCell with share_time_frequency_weights,
+// couple_input_forget_gates, frequency_skip == feature_size and a
+// concatenated state; dataflow decoded from save/g2k_mcr_model_val_0.ckpt-0
+// .meta (oracle/g2k_ref.py gridlstm_cell).  Rows are
+// independent; a row's frequency blocks are a chain (block k reads block
+// k - 1's c_freq, m_freq), so one lane owns one row and walks its blocks.
+// W / b / peepholes are wave-uniform (scalar loads).  Elementwise and
+// latency work on [rows, <= 32] tiles: no MFMA.
+// ---------------------------------------------------------------------------
+struct GridArgs {
+  const float* in;
+  const float* state;
+  const float* W;      // [FS + 2U, 3U]
+  const float* b;      // [3U]
+  const float* peep;   // [4, U] = (wIf, wIt, wOf, wOt) or NULL
+  float* out;          // [rows, K * 2U]
+  float* state_out;    // [rows, K * 2U]
+  int64_t rows, ld_in, ld_state;
+  int K;
+};
+
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+template <int U, int FS>
+__global__ void __launch_bounds__(256) g2k_gridlstm_kernel(GridArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= a.rows) return;
+  constexpr int NI = FS + 2 * U;
+  const float* xr = a.in + r * a.ld_in;
+  const float* sr = a.state + r * a.ld_state;
+  float* orow = a.out + r * (int64_t)(2 * U) * a.K;
+  float* srow = a.state_out + r * (int64_t)(2 * U) * a.K;
+  const bool peep = a.peep != nullptr;
+  float cf[U], mf[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) { cf[j] = 0.f; mf[j] = 0.f; }
+  for (int k = 0; k < a.K; ++k) {
+    float v[NI], ct[U];
+#pragma unroll
+    for (int i = 0; i < FS; ++i) v[i] = xr[k * FS + i];                 // x_k
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      ct[j] = sr[2 * U * k + j];                                         // c_time
+      v[FS + j] = sr[2 * U * k + U + j];                                 // m_time
+      v[FS + U + j] = mf[j];                                             // m_freq of block k - 1
+    }
+    float z[3 * U];
+#pragma unroll
+    for (int j = 0; j < 3 * U; ++j) {
+      float acc = a.b[j];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) acc = fmaf(v[i], a.W[i * 3 * U + j], acc);
+      z[j] = acc;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      float gi = z[j];
+      if (peep) gi += a.peep[j] * cf[j] + a.peep[U + j] * ct[j];
+      const float ig = sigmoid_f(gi);                                    // coupled: f = 1 - i
+      const float gg = tanhf(z[U + j]);
+      const float cfn = (1.f - ig) * cf[j] + ig * gg;
+      const float ctn = (1.f - ig) * ct[j] + ig * gg;
+      float go = z[2 * U + j];
+      if (peep) go += a.peep[2 * U + j] * cfn + a.peep[3 * U + j] * ctn;
+      const float og = sigmoid_f(go);
+      const float mfn = og * tanhf(cfn), mtn = og * tanhf(ctn);
+      srow[2 * U * k + j] = ctn;
+      srow[2 * U * k + U + j] = mtn;
+      orow[2 * U * k + j] = mtn;
+      orow[2 * U * k + U + j] = mfn;
+      cf[j] = cfn;
+      mf[j] = mfn;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Train mode (SURVEY.md §8(d) "--mode train", §8(e) gradient all-reduce).
+// The reference defines no loss or optimizer (SURVEY.md finding 5); the loss
+// here is half the squared error of the pred_path_band rows against the
+// targets the a9 errors use, over frames < n_frames and active, masked
+// pedestrians, differentiated through a2-a4 and a7 (the a8 recurrence does
+// not reach the predictions: Wr's gradient is exactly zero).  Restated in
+// float64 by oracle/g2k_ref.py scene_loss_grad (pinned by finite
+// differences).
+//
+// g2k_grad_kernel: grid (frame groups of GW, S), GW waves; wave w recomputes
+// frame (group * GW + w)'s forward and back-propagates it through a dozen
+// tiny products kept in its LDS scratch, one lane per output entry (every
+// wave runs the same step sequence, so steps are separated by workgroup
+// barriers).  The group's gradients are summed in wave order into the
+// (scene, group) row of a partial buffer; two fixed-order reduction passes
+// give the step's gradient.  Deterministic, no atomics.  VALU + LDS: each
+// product is at most 24 x 16 outputs over an 8..Nmax contraction — too small
+// for MFMA tiles to pay.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline int grad_params(int Nmax) { return 24 * Nmax + 496; }
+
+struct GradOff {
+  int wi, wii, wv, bv, wr, wc, wo;
+};
+__host__ __device__ inline GradOff grad_off(int Nmax) {   // g2k_weights order
+  GradOff o;
+  o.wi = 0;
+  o.wii = o.wi + Nmax * kD;
+  o.wv = o.wii + kD * kT;
+  o.bv = o.wv + kT * (kD + 2);
+  o.wr = o.bv + kD;
+  o.wc = o.wr + kT * 2;
+  o.wo = o.wc + kL2 * kT;
+  return o;
+}
+
+__host__ __device__ inline int grad_shared_floats(int Nmax) { return 26 * Nmax + 608; }
+__host__ __device__ inline int grad_scratch_floats(int Nmax) { return 32 * Nmax + 2084; }
+__host__ __device__ inline int grad_waves(int Nmax) { return Nmax > 128 ? 2 : 4; }
+constexpr int kGradSlices = 32;
+
+// one wave's LDS scratch in g2k_grad_kernel (floats)
+struct GradScratch {
+  float *B, *X, *U, *E, *C, *M, *dY, *dM, *dC, *dE, *dX, *dU, *gWc, *gWv, *gbv, *gWii, *loss;
+  __device__ GradScratch(float* p, int Nmax) {
+    B = p;    p += kT * Nmax;        // window norms [T][Nmax] (a2)
+    X = p;    p += (kD + 2) * kD;    // [X0; Ve]
+    U = p;    p += kT * kD;          // Bv @ Wi
+    E = p;    p += kT * kD;
+    C = p;    p += kT * kT;          // cost
+    M = p;    p += kL2 * kT;         // Wc @ cost
+    dY = p;   p += kL2 * Nmax;
+    dM = p;   p += kL2 * kT;
+    dC = p;   p += kT * kT;
+    dE = p;   p += kT * kD;
+    dX = p;   p += (kD + 2) * kD;
+    dU = p;   p += kT * kD;
+    gWc = p;  p += kL2 * kT;
+    gWv = p;  p += kT * (kD + 2);
+    gbv = p;  p += kD;
+    gWii = p; p += kD * kT;
+    loss = p;                        // {1/2 sum dY^2, count}
+  }
+};
+
+struct GradArgs {
+  g2k_dims d;
+  g2k_weights w;
+  const float *pos, *vislet, *G, *targets;
+  const int32_t *n_active, *n_frames;
+  const uint8_t* ped_mask;
+  float lambda;
+  float* part;   // [S * ngroup][P + 2]
+  int ngroup;
+};
+
+template <int GW>
+__global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
+  constexpr int NT = 64 * GW;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Nmax = a.d.Nmax, F = a.d.F, P = grad_params(Nmax);
+  const int s = blockIdx.y, grp = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+  const int nact = clampi(a.n_active[s], 0, Nmax);
+  const int nf = a.n_frames ? clampi(a.n_frames[s], 0, F) : F;
+  const int f = grp * GW + wv;
+  const bool act = f < nf;
+  float* sWi = smem;
+  float* sWo = sWi + Nmax * kD;
+  float* sWii = sWo + kT * Nmax;
+  float* sWv = sWii + kD * kT;
+  float* sbv = sWv + kT * (kD + 2);
+  float* sWc = sbv + kD;
+  float* sg = sWc + kL2 * kT;
+  float* sVis = sg + kD * kT;
+  float* scratch0 = smem + grad_shared_floats(Nmax);
+  const int PW = grad_scratch_floats(Nmax);
+  const GradScratch w(scratch0 + wv * PW, Nmax);
+  const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
+
+  for (int i = tid; i < Nmax * kD; i += NT) sWi[i] = a.w.Wi[i];
+  for (int i = tid; i < kT * Nmax; i += NT) sWo[i] = a.w.Wo[i];
+  for (int i = tid; i < kD * kT; i += NT) {
+    sWii[i] = a.w.Wii[i];
+    sg[i] = a.lambda * a.G[(size_t)s * kD * kT + i];
+  }
+  for (int i = tid; i < kT * (kD + 2); i += NT) sWv[i] = a.w.Wv[i];
+  for (int i = tid; i < kL2 * kT; i += NT) sWc[i] = a.w.Wc[i];
+  if (tid < kD) sbv[tid] = a.w.bv[tid];
+  for (int i = tid; i < 2 * Nmax; i += NT) sVis[i] = a.vislet[(size_t)s * 2 * Nmax + i];
+  for (int i = lane; i < kT * Nmax; i += 64) {                 // a2 window norms (train.py:76-85)
+    const int t = i / Nmax, n = i - t * Nmax;
+    float v = 0.f;
+    if (act && n < nact) {
+      const float2 p = *reinterpret_cast<const float2*>(
+          a.pos + (((size_t)s * a.d.W + (size_t)f * a.d.stride + t) * Nmax + n) * 2);
+      v = sqrtf(fmaf(p.x, p.x, p.y * p.y));
+    }
+    w.B[i] = v;
+  }
+  __syncthreads();
+  // forward (train.py:178-195, models/g2k_lstm_mcr.py:105-122)
+  for (int o = lane; o < (kT + 2) * kD; o += 64) {           // U = Bv @ Wi; Ve = vislet @ Wi
+    const int r = o >> 4, d = o & 15;
+    const float* src = r < kT ? w.B + r * Nmax : sVis + (r - kT) * Nmax;
+    float acc = 0.f;
+    for (int n = 0; n < nact; ++n) acc = fmaf(src[n], sWi[n * kD + d], acc);
+    if (r < kT) w.U[r * kD + d] = acc;
+    else w.X[(kD + r - kT) * kD + d] = acc;
+  }
+  __syncthreads();
+  for (int o = lane; o < kD * kD; o += 64) {                  // X0 = Wii @ U
+    const int r = o >> 4, d = o & 15;
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < kT; ++t) acc = fmaf(sWii[r * kT + t], w.U[t * kD + d], acc);
+    w.X[o] = acc;
+  }
+  __syncthreads();
+  for (int o = lane; o < kT * kD; o += 64) {                  // E = Wv @ X + bv
+    const int t = o >> 4, d = o & 15;
+    float acc = sbv[d];
+#pragma unroll
+    for (int c = 0; c < kD + 2; ++c) acc = fmaf(sWv[t * (kD + 2) + c], w.X[c * kD + d], acc);
+    w.E[o] = acc;
+  }
+  __syncthreads();
+  {                                                           // cost = E @ (lambda G)
+    const int t = lane >> 3, u = lane & 7;
+    float acc = 0.f;
+#pragma unroll
+    for (int d = 0; d < kD; ++d) acc = fmaf(w.E[t * kD + d], sg[d * kT + u], acc);
+    w.C[lane] = acc;
+  }
+  __syncthreads();
+  for (int o = lane; o < kL2 * kT; o += 64) {                 // M = Wc @ cost
+    const int r = o >> 3, t = o & 7;
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < kT; ++u) acc = fmaf(sWc[r * kT + u], w.C[u * kT + t], acc);
+    w.M[o] = acc;
+  }
+  __syncthreads();
+  // dY = Y - target on active, masked pedestrians (Y = M @ Wo, :122-124)
+  float lsum = 0.f;
+  for (int o = lane; o < kL2 * Nmax; o += 64) {
+    const int r = o / Nmax, n = o - r * Nmax;
+    float dy = 0.f;
+    if (act && n < nact && (pm ? pm[n] != 0 : true)) {
+      float y = 0.f;
+#pragma unroll
+      for (int t = 0; t < kT; ++t) y = fmaf(w.M[r * kT + t], sWo[t * Nmax + n], y);
+      const int l = r < kL ? r : r - kL;
+      dy = y - a.targets[((((size_t)s * F + f) * Nmax + n) * kL + l) * 2 + (r < kL ? 0 : 1)];
+      lsum = fmaf(dy, dy, lsum);
+    }
+    w.dY[o] = dy;
+  }
+  float cnt = 0.f;
+  for (int n = lane; n < Nmax; n += 64) cnt += (act && n < nact && (pm ? pm[n] != 0 : true)) ? 1.f : 0.f;
+  lsum = wave_sum(lsum);
+  cnt = wave_sum(cnt);
+  if (lane == 0) {
+    w.loss[0] = 0.5f * lsum;
+    w.loss[1] = cnt;
+  }
+  __syncthreads();
+  // backward
+  for (int o = lane; o < kL2 * kT; o += 64) {                 // dM = dY @ Wo^T
+    const int r = o >> 3, t = o & 7;
+    float acc = 0.f;
+    for (int n = 0; n < nact; ++n) acc = fmaf(w.dY[r * Nmax + n], sWo[t * Nmax + n], acc);
+    w.dM[o] = acc;
+  }
+  __syncthreads();
+  for (int o = lane; o < kT * kT + kL2 * kT; o += 64) {
+    if (o < kT * kT) {                                        // dcost = Wc^T @ dM
+      const int u = o >> 3, t = o & 7;
+      float acc = 0.f;
+      for (int r = 0; r < kL2; ++r) acc = fmaf(sWc[r * kT + u], w.dM[r * kT + t], acc);
+      w.dC[o] = acc;
+    } else {                                                  // dWc = dM @ cost^T
+      const int p = o - kT * kT, r = p >> 3, u = p & 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < kT; ++t) acc = fmaf(w.dM[r * kT + t], w.C[u * kT + t], acc);
+      w.gWc[p] = acc;
+    }
+  }
+  __syncthreads();
+  for (int o = lane; o < kT * kD; o += 64) {                  // dE = dcost @ (lambda G)^T
+    const int t = o >> 4, d = o & 15;
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < kT; ++u) acc = fmaf(w.dC[t * kT + u], sg[d * kT + u], acc);
+    w.dE[o] = acc;
+  }
+  __syncthreads();
+  for (int o = lane; o < (kD + 2) * kD + kT * (kD + 2) + kD; o += 64) {
+    if (o < (kD + 2) * kD) {                                  // dX = Wv^T @ dE
+      const int c = o >> 4, d = o & 15;
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < kT; ++t) acc = fmaf(sWv[t * (kD + 2) + c], w.dE[t * kD + d], acc);
+      w.dX[o] = acc;
+    } else if (o < (kD + 2) * kD + kT * (kD + 2)) {           // dWv = dE @ X^T
+      const int p = o - (kD + 2) * kD, t = p / (kD + 2), c = p - t * (kD + 2);
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < kD; ++d) acc = fmaf(w.dE[t * kD + d], w.X[c * kD + d], acc);
+      w.gWv[p] = acc;
+    } else {                                                  // dbv = column sums of dE
+      const int d = o - (kD + 2) * kD - kT * (kD + 2);
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < kT; ++t) acc += w.dE[t * kD + d];
+      w.gbv[d] = acc;
+    }
+  }
+  __syncthreads();
+  for (int o = lane; o < 2 * kT * kD; o += 64) {
+    if (o < kT * kD) {                                        // dU = Wii^T @ dX0
+      const int t = o >> 4, d = o & 15;
+      float acc = 0.f;
+#pragma unroll
+      for (int r = 0; r < kD; ++r) acc = fmaf(sWii[r * kT + t], w.dX[r * kD + d], acc);
+      w.dU[o] = acc;
+    } else {                                                  // dWii = dX0 @ U^T
+      const int p = o - kT * kD, r = p >> 3, t = p & 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < kD; ++d) acc = fmaf(w.dX[r * kD + d], w.U[t * kD + d], acc);
+      w.gWii[p] = acc;
+    }
+  }
+  __syncthreads();
+  // this group's gradient row, frames summed in wave order
+  const GradOff go = grad_off(Nmax);
+  float* row = a.part + ((size_t)s * a.ngroup + grp) * (size_t)(P + 2);
+  for (int p = tid; p < P + 2; p += NT) {
+    float v = 0.f;
+    for (int wi = 0; wi < GW; ++wi) {
+      const GradScratch x(scratch0 + wi * PW, Nmax);
+      float c = 0.f;
+      if (p < go.wii) {                                       // dWi = Bv^T @ dU + vislet^T @ dVe
+        const int n = p >> 4, d = p & 15;
+        if (n < nact) {
+#pragma unroll
+          for (int t = 0; t < kT; ++t) c = fmaf(x.B[t * Nmax + n], x.dU[t * kD + d], c);
+          c = fmaf(sVis[n], x.dX[kD * kD + d], c);
+          c = fmaf(sVis[Nmax + n], x.dX[(kD + 1) * kD + d], c);
+        }
+      } else if (p < go.wv) {
+        c = x.gWii[p - go.wii];
+      } else if (p < go.bv) {
+        c = x.gWv[p - go.wv];
+      } else if (p < go.wr) {
+        c = x.gbv[p - go.bv];
+      } else if (p < go.wc) {
+        c = 0.f;                                              // Wr does not reach pred
+      } else if (p < go.wo) {
+        c = x.gWc[p - go.wc];
+      } else if (p < P) {                                     // dWo = M^T @ dY
+        const int q = p - go.wo, t = q / Nmax, n = q - t * Nmax;
+        for (int r = 0; r < kL2; ++r) c = fmaf(x.M[r * kT + t], x.dY[r * Nmax + n], c);
+      } else {
+        c = x.loss[p - P];
+      }
+      v += c;
+    }
+    row[p] = v;
+  }
+}
+
+// pass 1: slice k sums rows k, k + kGradSlices, ... (fixed order)
+__global__ void __launch_bounds__(256) g2k_grad_reduce1_kernel(const float* __restrict__ part,
+                                                               float* __restrict__ red, int rows,
+                                                               int width) {
+  const int p = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y;
+  if (p >= width) return;
+  float acc = 0.f;
+#pragma unroll 4
+  for (int r = k; r < rows; r += kGradSlices) acc += part[(size_t)r * width + p];
+  red[(size_t)k * width + p] = acc;
+}
+
+// pass 2: the slices in order
+__global__ void __launch_bounds__(256) g2k_grad_reduce2_kernel(const float* __restrict__ red,
+                                                               float* __restrict__ grad, int width) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= width) return;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < kGradSlices; ++k) acc += red[(size_t)k * width + p];
+  grad[p] = acc;
+}
+
+// Optimizer step (argParser.py:38-47: grad_clip, learning_rate, decay_rate):
+// g = grad / count, clipped by global norm (g * clip / max(||g||, clip)),
+// then RMSProp (ms = decay ms + (1 - decay) g^2; p -= lr g / sqrt(ms +
+// 1e-10), TF RMSPropOptimizer without momentum) or SGD (ms NULL).  One
+// workgroup: the norm is a fixed-order block reduction.
+__global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ params,
+                                                          float* __restrict__ ms,
+                                                          const float* __restrict__ grad, int n,
+                                                          float lr, float decay, float clip) {
+  __shared__ float red[16];
+  const int tid = threadIdx.x;
+  const float inv = 1.0f / fmaxf(grad[n + 1], 1.0f);
+  float ss = 0.f;
+  for (int i = tid; i < n; i += 1024) {
+    const float g = grad[i] * inv;
+    ss = fmaf(g, g, ss);
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) tot += red[w];
+  const float nrm = sqrtf(tot);
+  const float scale = clip > 0.f ? inv * (clip / fmaxf(nrm, clip)) : inv;
+  for (int i = tid; i < n; i += 1024) {
+    const float g = grad[i] * scale;
+    if (ms) {
+      const float m = fmaf(decay, ms[i], (1.f - decay) * g * g);
+      ms[i] = m;
+      params[i] -= lr * g / sqrtf(m + 1e-10f);
+    } else {
+      params[i] = fmaf(-lr, g, params[i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host-side validation / geometry
 // ---------------------------------------------------------------------------
 int validate_common(const g2k_dims* d, bool need_F) {
@@ -2598,6 +3031,115 @@ int g2k_eval_rln_ngh_f32(const float* adj, float* out, int64_t rows, int32_t col
   hipLaunchKernelGGL(g2k_row_softmax_kernel, dim3((unsigned)rows), dim3(64), 0,
                      (hipStream_t)stream, adj, out, cols);
   return check_launch("g2k_eval_rln_ngh_f32");
+}
+
+int g2k_gridlstm_f32(const float* in, int64_t ld_in, const float* state, int64_t ld_state,
+                     const float* W, const float* b, const float* peep, float* out,
+                     float* state_out, int64_t rows, int32_t blocks, int32_t feature_size,
+                     int32_t num_units, void* stream) {
+  if (!in || !state || !W || !b || !out || !state_out)
+    return set_err(G2K_EINVAL, "a required buffer pointer is NULL");
+  if (rows < 0 || blocks < 1 || feature_size < 1 || num_units < 1)
+    return set_err(G2K_EINVAL, "rows=%lld blocks=%d feature_size=%d num_units=%d", (long long)rows,
+                   blocks, feature_size, num_units);
+  const int64_t w_out = (int64_t)blocks * 2 * num_units;
+  if (ld_in < (int64_t)blocks * feature_size || ld_state < w_out)
+    return set_err(G2K_EINVAL, "row pitch too small (ld_in=%lld, ld_state=%lld)", (long long)ld_in,
+                   (long long)ld_state);
+  if (state_out == state && ld_state != w_out)
+    return set_err(G2K_EINVAL, "state_out may alias state only when ld_state == blocks*2*num_units");
+  const bool ok_u = num_units == 1 || num_units == 2 || num_units == 4;
+  const bool ok_f = feature_size == 2 || feature_size == 4 || feature_size == 8;
+  if (!ok_u || !ok_f)
+    return set_err(G2K_EUNSUPPORTED, "num_units=%d feature_size=%d (built: units 1/2/4, features 2/4/8)",
+                   num_units, feature_size);
+  if (rows == 0) return G2K_OK;
+  GridArgs a;
+  a.in = in; a.state = state; a.W = W; a.b = b; a.peep = peep; a.out = out; a.state_out = state_out;
+  a.rows = rows; a.ld_in = ld_in; a.ld_state = ld_state; a.K = blocks;
+  const dim3 g((unsigned)((rows + 255) / 256)), blk(256);
+  hipStream_t st = (hipStream_t)stream;
+  const int key = num_units * 16 + feature_size;
+  switch (key) {
+    case 1 * 16 + 2: hipLaunchKernelGGL((g2k_gridlstm_kernel<1, 2>), g, blk, 0, st, a); break;
+    case 1 * 16 + 4: hipLaunchKernelGGL((g2k_gridlstm_kernel<1, 4>), g, blk, 0, st, a); break;
+    case 1 * 16 + 8: hipLaunchKernelGGL((g2k_gridlstm_kernel<1, 8>), g, blk, 0, st, a); break;
+    case 2 * 16 + 2: hipLaunchKernelGGL((g2k_gridlstm_kernel<2, 2>), g, blk, 0, st, a); break;
+    case 2 * 16 + 4: hipLaunchKernelGGL((g2k_gridlstm_kernel<2, 4>), g, blk, 0, st, a); break;
+    case 2 * 16 + 8: hipLaunchKernelGGL((g2k_gridlstm_kernel<2, 8>), g, blk, 0, st, a); break;
+    case 4 * 16 + 2: hipLaunchKernelGGL((g2k_gridlstm_kernel<4, 2>), g, blk, 0, st, a); break;
+    case 4 * 16 + 4: hipLaunchKernelGGL((g2k_gridlstm_kernel<4, 4>), g, blk, 0, st, a); break;
+    default:         hipLaunchKernelGGL((g2k_gridlstm_kernel<4, 8>), g, blk, 0, st, a); break;
+  }
+  return check_launch("g2k_gridlstm_f32");
+}
+
+int64_t g2k_grad_size(const g2k_dims* d) {
+  if (validate_common(d, false) != G2K_OK) return -1;
+  return grad_params(d->Nmax);
+}
+
+int64_t g2k_grad_workspace_bytes(const g2k_dims* d) {
+  if (validate_common(d, true) != G2K_OK) return -1;
+  const int GW = grad_waves(d->Nmax);
+  const int64_t ngroup = (d->F + GW - 1) / GW;
+  return ((int64_t)d->S * ngroup + kGradSlices) * (grad_params(d->Nmax) + 2) * 4;
+}
+
+int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
+                      const float* vislet, const float* G, const float* targets,
+                      const int32_t* n_active, const int32_t* n_frames, const uint8_t* ped_mask,
+                      float lambda, float* grad, void* workspace, int64_t workspace_bytes,
+                      void* stream) {
+  int rc = validate_common(d, true);
+  if (rc) return rc;
+  if ((rc = validate_weights(w, true))) return rc;
+  if (d->stride < 0) return set_err(G2K_EINVAL, "stride=%d < 0", d->stride);
+  if (d->F > 0 && d->W < (d->F - 1) * d->stride + kT)
+    return set_err(G2K_EINVAL, "W=%d < (F-1)*stride + T = %d", d->W, (d->F - 1) * d->stride + kT);
+  if (!pos || !vislet || !G || !targets || !n_active || !grad)
+    return set_err(G2K_EINVAL, "a required buffer pointer is NULL");
+  if (((uintptr_t)pos & 7u) != 0) return set_err(G2K_EINVAL, "pos must be 8-byte aligned");
+  const int64_t need = g2k_grad_workspace_bytes(d);
+  if (!workspace || workspace_bytes < need)
+    return set_err(G2K_EINVAL, "workspace of %lld bytes needed (got %lld)", (long long)need,
+                   (long long)workspace_bytes);
+  const int GW = grad_waves(d->Nmax);
+  const int ngroup = (d->F + GW - 1) / GW;
+  const int width = grad_params(d->Nmax) + 2;
+  hipStream_t st = (hipStream_t)stream;
+  if (d->S == 0 || ngroup == 0) {
+    if (hipMemsetAsync(grad, 0, (size_t)width * 4, st) != hipSuccess)
+      return set_err(G2K_ELAUNCH, "g2k_step_grad_f32: memset failed");
+    return G2K_OK;
+  }
+  const size_t lds = (size_t)4 * (grad_shared_floats(d->Nmax) + GW * grad_scratch_floats(d->Nmax));
+  if (lds > 160 * 1024) return set_err(G2K_ELDS, "Nmax=%d needs %zu bytes of LDS", d->Nmax, lds);
+  GradArgs a;
+  a.d = *d; a.w = *w; a.pos = pos; a.vislet = vislet; a.G = G; a.targets = targets;
+  a.n_active = n_active; a.n_frames = n_frames; a.ped_mask = ped_mask; a.lambda = lambda;
+  a.part = static_cast<float*>(workspace); a.ngroup = ngroup;
+  float* red = a.part + (size_t)d->S * ngroup * width;
+  if (GW == 4)
+    hipLaunchKernelGGL((g2k_grad_kernel<4>), dim3(ngroup, d->S), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL((g2k_grad_kernel<2>), dim3(ngroup, d->S), dim3(128), lds, st, a);
+  if ((rc = check_launch("g2k_step_grad_f32/grad"))) return rc;
+  const unsigned gx = (unsigned)((width + 255) / 256);
+  hipLaunchKernelGGL(g2k_grad_reduce1_kernel, dim3(gx, kGradSlices), dim3(256), 0, st, a.part, red,
+                     d->S * ngroup, width);
+  hipLaunchKernelGGL(g2k_grad_reduce2_kernel, dim3(gx), dim3(256), 0, st, red, grad, width);
+  return check_launch("g2k_step_grad_f32/reduce");
+}
+
+int g2k_update_f32(float* params, float* ms, const float* grad, int64_t n_params, float lr,
+                   float decay, float grad_clip, void* stream) {
+  if (!params || !grad || n_params < 0 || n_params > (1 << 30))
+    return set_err(G2K_EINVAL, "bad arguments");
+  if (n_params == 0) return G2K_OK;
+  hipLaunchKernelGGL(g2k_update_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, params, ms, grad,
+                     (int)n_params, lr, decay, grad_clip);
+  return check_launch("g2k_update_f32");
 }
 
 }  // extern "C"

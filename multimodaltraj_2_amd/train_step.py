@@ -1,0 +1,148 @@
+"""--mode train: the reference-mode step plus a
+loss, its gradient, ONE all-reduce and an optimizer update per batch.
+
+The reference has no loss, gradient or optimizer for g2k_lstm_mcr (SURVEY.md
+finding 5: its training loop re-initialises weights and fetches fed tensors);
+this mode is the build's, for the north star's "RCCL all-reduce of
+gradients".  loss = 1/2 the squared error of the pred_path_band rows against
+the targets the ADE/FDE use; the gradient comes from g2k_step_grad_f32
+(checked against the float64 oracle ``scene_loss_grad``, itself pinned by
+finite differences; unpinned against the reference, which has none).  One
+flat [P + 2] buffer (gradient sums, loss, count) is all-reduced per step —
+RCCL over xGMI under the nccl backend, 5.1 KB at Nmax = 32 — then every rank
+applies the same update (RMSProp with global-norm clipping, argParser.py:38-47
+defaults), so the replicas stay identical.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .frame_step import (HIDDEN_LEN, LAMBDA, OBS_LEN, PRED_LEN, G2KParams, StepPlan, _check_dev,
+                         _ptr, _stream)
+
+GRAD_ORDER = ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo")   # g2k_weights order
+LEARNING_RATE = 0.005    # argParser.py:43
+DECAY_RATE = 0.95        # argParser.py:46 (RMSProp)
+GRAD_CLIP = 10.0         # argParser.py:40
+
+
+def grad_size(nmax: int) -> int:
+    """Floats in one parameter vector (g2k_grad_size): 24 * Nmax + 496."""
+    return 24 * int(nmax) + 496
+
+
+def flat_params(params: G2KParams):
+    """Copy ``params`` into one flat device buffer in gradient layout and
+    return (flat, G2KParams of views into it), so one update kernel and one
+    all-reduce cover every parameter."""
+    flat = torch.cat([getattr(params, k).reshape(-1) for k in GRAD_ORDER]).contiguous()
+    views, o = {}, 0
+    for k in GRAD_ORDER:
+        t = getattr(params, k)
+        views[k] = flat[o:o + t.numel()].view(t.shape)
+        o += t.numel()
+    return flat, G2KParams(**views)
+
+
+class GradPlan:
+    """A validated launch of ``g2k_step_grad_f32`` bound to fixed buffers;
+    ``run()`` returns grad [P + 2] = (gradient sums, loss, count)."""
+
+    def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, *, n_frames=None,
+                 ped_mask=None, stride=1, lam=LAMBDA, grad=None, stream=None):
+        lib = _lib.load()
+        dev = pos.device
+        if dev.type != "cuda":
+            raise ValueError("the gradient runs on the GPU only (no CPU fallback)")
+        S, W, Nmax, two = pos.shape
+        if two != 2:
+            raise ValueError(f"pos: last dim {two}, expected 2")
+        F = int(targets.shape[1])
+        params.check(dev)
+        if params.nmax != Nmax:
+            raise ValueError(f"params Nmax={params.nmax} but pos Nmax={Nmax}")
+        exp = dict(pos=(S, W, Nmax, 2), vislet=(S, 2, Nmax), G=(S, HIDDEN_LEN, OBS_LEN),
+                   targets=(S, F, Nmax, PRED_LEN, 2))
+        for k, t in dict(pos=pos, vislet=vislet, G=G, targets=targets).items():
+            if tuple(t.shape) != exp[k]:
+                raise ValueError(f"{k}: shape {tuple(t.shape)}, expected {exp[k]}")
+            _check_dev(k, t, dev, torch.float32)
+        _check_dev("n_active", n_active, dev, torch.int32)
+        if n_frames is not None:
+            _check_dev("n_frames", n_frames, dev, torch.int32)
+        if ped_mask is not None:
+            _check_dev("ped_mask", ped_mask, dev, torch.uint8)
+        d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 64, Nmax, W, stride)
+        P = int(lib.g2k_grad_size(ctypes.byref(d)))
+        nws = int(lib.g2k_grad_workspace_bytes(ctypes.byref(d)))
+        if P < 0 or nws < 0:
+            _lib.check("g2k_grad_size", -1)
+        self.P = P
+        self.grad = grad if grad is not None else torch.empty(P + 2, device=dev,
+                                                              dtype=torch.float32)
+        self._ws = torch.empty(max(nws, 256), dtype=torch.uint8, device=dev)
+        w = params.abi()
+        self._fn = lib.g2k_step_grad_f32
+        self._args = (ctypes.byref(d), ctypes.byref(w), _ptr(pos), _ptr(vislet), _ptr(G),
+                      _ptr(targets), _ptr(n_active), _ptr(n_frames), _ptr(ped_mask),
+                      ctypes.c_float(lam), self.grad.data_ptr(), self._ws.data_ptr(), nws,
+                      _stream(stream))
+        self._keep = (d, w, params, pos, vislet, G, targets, n_active, n_frames, ped_mask)
+
+    def run(self) -> torch.Tensor:
+        rc = self._fn(*self._args)
+        if rc:
+            _lib.check("g2k_step_grad_f32", rc)
+        return self.grad
+
+
+def optimizer_update(flat, grad, *, lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP,
+                     ms=None, stream=None):
+    """params -= step(grad[:P] / grad[P+1]) (g2k_update_f32): RMSProp when
+    ``ms`` (the mean-square buffer, [P]) is given, else SGD."""
+    lib = _lib.load()
+    n = flat.numel()
+    if grad.numel() != n + 2:
+        raise ValueError(f"grad must have {n + 2} entries")
+    rc = lib.g2k_update_f32(flat.data_ptr(), None if ms is None else ms.data_ptr(),
+                            grad.data_ptr(), n, float(lr), float(decay), float(grad_clip),
+                            _stream(stream))
+    _lib.check("g2k_update_f32", rc)
+
+
+class TrainStep:
+    """One train-mode step over fixed device buffers: the fused reference
+    step (pred, h, ADE/FDE sums), the loss gradient, the all-reduce of the
+    flat gradient across ranks (when a process group is up), the update."""
+
+    def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
+                 lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,
+                 n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None):
+        self.flat, self.params = flat_params(params)
+        self.fwd = StepPlan(self.params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
+                            ped_mask=ped_mask, stride=stride, lam=lam, out=out)
+        self.gradplan = GradPlan(self.params, pos, vislet, G, targets, n_active,
+                                 n_frames=n_frames, ped_mask=ped_mask, stride=stride, lam=lam)
+        self.ms = torch.zeros_like(self.flat) if rmsprop else None
+        self.lr, self.decay, self.grad_clip = lr, decay, grad_clip
+        self.group = group
+        self.world = (dist.get_world_size(group)
+                      if dist.is_available() and dist.is_initialized() else 1)
+
+    @property
+    def out(self):
+        return self.fwd.out
+
+    def run(self) -> torch.Tensor:
+        """Returns the (all-rank) [P + 2] buffer: gradient sums, loss, count."""
+        self.fwd.run()
+        g = self.gradplan.run()
+        if self.world > 1:
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
+        optimizer_update(self.flat, g, lr=self.lr, decay=self.decay, grad_clip=self.grad_clip,
+                         ms=self.ms)
+        return g

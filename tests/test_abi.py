@@ -80,3 +80,28 @@ def test_zero_scenes_is_a_noop():
     rc = lib.g2k_step_fused_f32(ctypes.byref(_dims(S=0)), ctypes.byref(w), p, p, p, p, p, None,
                                 None, p, p, p, p, None, None, 5e-4, p, 0, None)
     assert rc == 0
+
+
+def test_gridlstm_and_train_entry_points_validate():
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)
+    # g2k_gridlstm_f32(in, ld_in, state, ld_state, W, b, peep, out, state_out, rows, K, fs, u, s)
+    assert lib.g2k_gridlstm_f32(None, 16, p, 16, p, p, None, p, p, 4, 4, 4, 2, None) == -1
+    assert lib.g2k_gridlstm_f32(p, 15, p, 16, p, p, None, p, p, 4, 4, 4, 2, None) == -1
+    assert lib.g2k_gridlstm_f32(p, 16, p, 24, p, p, None, p, p, 4, 4, 4, 3, None) == -4
+    # state_out aliases state with a wider pitch
+    assert lib.g2k_gridlstm_f32(p, 16, p, 20, p, p, None, p, p, 4, 4, 4, 2, None) == -1
+    assert lib.g2k_gridlstm_f32(p, 16, p, 16, p, p, None, p, p, 0, 4, 4, 2, None) == 0
+    d = _dims()
+    assert lib.g2k_grad_size(ctypes.byref(d)) == 24 * 32 + 496
+    need = lib.g2k_grad_workspace_bytes(ctypes.byref(d))
+    assert need == (2 * 5 + 32) * (24 * 32 + 498) * 4
+    w = _lib.G2KWeights(*([p] * 7))
+    rc = lib.g2k_step_grad_f32(ctypes.byref(d), ctypes.byref(w), p, p, p, p, p, None, None, 5e-4,
+                               p, p, need - 4, None)
+    assert rc == -1 and b"workspace" in lib.g2k_last_error()
+    rc = lib.g2k_step_grad_f32(ctypes.byref(_dims(T=9)), ctypes.byref(w), p, p, p, p, p, None,
+                               None, 5e-4, p, p, need, None)
+    assert rc == -4
+    assert lib.g2k_update_f32(None, None, p, 10, 0.1, 0.9, 10.0, None) == -1
+    assert lib.g2k_update_f32(p, None, p, 0, 0.1, 0.9, 10.0, None) == 0

@@ -22,7 +22,9 @@ Also decodes the TF tensor-bundle checkpoint
 save/g2k_mcrAttn_model_kfold_train_4_0.ckpt-79 (.index SSTable of
 BundleEntryProto + raw .data) and stores, for every model copy, weight_c,
 cost and the forward Variable holding weight_c @ cost (models/g2k_lstm_mcr.py:122)
-as tests/golden/ckpt_mcr_attn.npz — a known-answer test for the oracle.
+as tests/golden/ckpt_mcr_attn.npz — a known-answer test for the oracle —
+and the GridLSTMCell weights of save/g2k_mcr_model_val_0.ckpt-0 as
+tests/golden/ckpt_gridlstm.npz.
 """
 from __future__ import annotations
 
@@ -225,6 +227,24 @@ def make_ckpt_fixture():
     return n, len(t)
 
 
+def make_gridlstm_fixture():
+    """GridLSTMCell weights (helper.py:31-39) from the reference's own
+    checkpoint save/g2k_mcr_model_val_0.ckpt-0: W_f_0_0 [8,6], B_f_0 [6] and
+    the four peephole diagonals [2] — realistic weights for the a6 kernel's
+    tests (its outputs stay unpinned: no reference run exists)."""
+    t = read_bundle(os.path.join(REF, "save", "g2k_mcr_model_val_0.ckpt-0"))
+    out, names = {}, []
+    for key, suf in (("W", "W_f_0_0"), ("b", "B_f_0"), ("wIf", "W_I_diag_freqf_0"),
+                     ("wIt", "W_I_diag_freqt_0"), ("wOf", "W_O_diag_freqf_0"),
+                     ("wOt", "W_O_diag_freqt_0")):
+        ks = sorted(k for k in t if k.endswith(suf))
+        names.append(ks[0])
+        out[key] = t[ks[0]]
+    out["names"] = np.array(names)
+    np.savez_compressed(os.path.join(OUT, "ckpt_gridlstm.npz"), **out)
+    return names
+
+
 def main():
     if not os.path.isdir(REF):
         print("no /root/reference here: fixtures are committed, nothing to do")
@@ -234,6 +254,7 @@ def main():
         rec = make_data_fixture(name, rel)
         print(name, {k: np.shape(v) for k, v in rec.items() if k.startswith("b0")})
     print("checkpoint pairs (weight_c @ cost == stored Variable):", make_ckpt_fixture())
+    print("gridlstm weights:", make_gridlstm_fixture())
 
 
 if __name__ == "__main__":
