@@ -71,6 +71,41 @@ def cpu_baseline(b, params_np, budget_s=12.0):
                        f"(float64 NumPy oracle, 1 thread, {dt:.1f} s)")
 
 
+def time_train(args, params, t, dev, dist, S, F, world):
+    """--mode train: the same step plus loss gradient, ONE
+    all-reduce of the flat [P + 2] gradient buffer across ranks (RCCL under
+    the nccl backend) and the RMSProp update (multimodaltraj_2_amd/train_step.py).
+    Timed like the reference-mode step: barrier + synchronize on both sides,
+    max over ranks."""
+    from multimodaltraj_2_amd.train_step import TrainStep
+    step = TrainStep(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+    for _ in range(args.warmup):
+        step.run()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g = step.run()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        e = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    gl = g.double().cpu().numpy()
+    return {"metric": "frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + L2 loss gradient + "
+                      "gradient all-reduce + RMSProp update",
+            "value": S * F * world * args.steps / el, "unit": "frames/s",
+            "ms_per_step": el / args.steps * 1e3, "allreduce_bytes": int(g.numel() * 4),
+            "loss_per_prediction_last_step": float(gl[-2] / max(gl[-1], 1.0)),
+            "optimizer": "RMSProp lr 0.005 decay 0.95, global-norm clip 10 (argParser.py:38-47)"}
+
+
 def load_pmc(config):
     p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(p):
@@ -91,6 +126,7 @@ def main():
     ap.add_argument("--scenes", type=int, default=0, help="override scenes per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-train", action="store_true", help="skip the --mode train timing")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,6 +200,8 @@ def main():
     achieved = abytes / kern_s / 1e9
     pmc = load_pmc(args.config)
 
+    train = None if args.no_train else time_train(args, params, t, dev, dist, S, F, world)
+
     if rank == 0:
         cpu = None if args.no_cpu_baseline or world > 1 else \
             cpu_baseline(b, params.numpy(), budget_s=args.cpu_budget)
@@ -191,6 +229,7 @@ def main():
             "cpu_baseline": cpu,
             "ade_fde_all_ranks": {"ADE": float(m[0] / max(m[1], 1)),
                                   "FDE_frob_per_frame": float(np.sqrt(m[2]) / max(m[5], 1))},
+            "train_mode": train,
         }
         print(json.dumps(line))
     if dist is not None:

@@ -21,6 +21,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
+from .dist import allreduce_grad
 from .frame_step import (HIDDEN_LEN, LAMBDA, OBS_LEN, PRED_LEN, G2KParams, StepPlan, _check_dev,
                          _ptr, _stream)
 
@@ -142,7 +143,7 @@ class TrainStep:
         self.fwd.run()
         g = self.gradplan.run()
         if self.world > 1:
-            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
+            allreduce_grad(g, self.group)
         optimizer_update(self.flat, g, lr=self.lr, decay=self.decay, grad_clip=self.grad_clip,
                          ms=self.ms)
         return g

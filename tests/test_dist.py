@@ -10,7 +10,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from multimodaltraj_2_amd.dist import global_errors, reduce_metrics, shard_scenes
+from multimodaltraj_2_amd.dist import allreduce_grad, global_errors, reduce_metrics, shard_scenes
 
 
 def _port():
@@ -74,3 +74,50 @@ def test_two_rank_gloo_metric_reduction():
     np.testing.assert_allclose(got, want, rtol=1e-12)
     ade, fde = global_errors(torch.tensor(got))
     assert np.isfinite(ade) and np.isfinite(fde)
+
+
+def _scene_grads(S, lo, hi):
+    """Flat [P + 2] train-mode buffer (gradient sums, loss, count) of scenes
+    [lo, hi) from the float64 oracle (stands in for g2k_step_grad_f32)."""
+    from multimodaltraj_2_amd.synthetic import make_batch
+    from oracle import g2k_ref as ref
+    b = make_batch(S, 16, 64, F=3, seed=12)
+    rng = np.random.default_rng(0)
+    shapes = dict(Wi=(16, 16), Wii=(16, 8), Wv=(8, 18), bv=(16,), Wr=(8, 2), Wc=(24, 8), Wo=(8, 16))
+    w = {k: rng.standard_normal(s) for k, s in shapes.items()}
+    flat = np.zeros(24 * 16 + 498)
+    for s in range(lo, hi):
+        loss, cnt, g = ref.scene_loss_grad(b.pos[s], b.vislet[s], b.G[s], w, b.targets[s],
+                                           b.n_active[s], n_frames=b.F, lam=0.05)
+        flat[:-2] += np.concatenate([g[k].reshape(-1) for k in ref.GRAD_ORDER])
+        flat[-2] += loss
+        flat[-1] += cnt
+    return torch.tensor(flat, dtype=torch.float64)
+
+
+def _grad_worker(rank, world, port, S, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_scenes(S, rank, world)
+    g = allreduce_grad(_scene_grads(S, lo, hi))
+    q.put((rank, g.numpy()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_gradient_allreduce():
+    """Train mode: each rank's shard gradient, summed by the one all-reduce,
+    equals the whole-batch gradient on every rank (identical updates)."""
+    S, world = 5, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, S, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = _scene_grads(S, 0, S).numpy()
+    for r in range(world):
+        np.testing.assert_allclose(got[r], want, rtol=1e-12, atol=1e-12)
