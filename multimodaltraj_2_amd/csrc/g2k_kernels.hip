@@ -2384,22 +2384,27 @@ __host__ __device__ inline GradOff grad_off(int Nmax) {   // g2k_weights order
   return o;
 }
 
-__host__ __device__ inline int grad_shared_floats(int Nmax) { return 26 * Nmax + 608; }
-__host__ __device__ inline int grad_scratch_floats(int Nmax) { return 32 * Nmax + 2084; }
-__host__ __device__ inline int grad_waves(int Nmax) { return Nmax > 128 ? 2 : 4; }
+// rows that lanes walk in parallel (window norms, dY, Wo, vislet) have the
+// odd pitch Nmax + 1, so lanes on different rows hit different LDS banks
+__host__ __device__ inline int grad_shared_floats(int Nmax) { return 26 * Nmax + 618; }
+__host__ __device__ inline int grad_scratch_floats(int Nmax) { return 72 * Nmax + 2116; }
+__host__ __device__ inline int grad_waves(int Nmax) { return Nmax > 128 ? 1 : (Nmax > 64 ? 2 : 4); }
 constexpr int kGradSlices = 32;
 
 // one wave's LDS scratch in g2k_grad_kernel (floats)
 struct GradScratch {
-  float *B, *X, *U, *E, *C, *M, *dY, *dM, *dC, *dE, *dX, *dU, *gWc, *gWv, *gbv, *gWii, *loss;
+  float *pos, *tgt, *B, *X, *U, *E, *C, *M, *dY, *dM, *dC, *dE, *dX, *dU, *gWc, *gWv, *gbv, *gWii,
+      *loss;
   __device__ GradScratch(float* p, int Nmax) {
-    B = p;    p += kT * Nmax;        // window norms [T][Nmax] (a2)
+    pos = p;  p += kT * 2 * Nmax;    // the frame's raw position window (LDS-DMA)
+    tgt = p;  p += kL2 * Nmax;       // the frame's targets [Nmax][L][2] (LDS-DMA)
+    B = p;    p += kT * (Nmax + 1);  // window norms [T][Nmax + 1] (a2)
     X = p;    p += (kD + 2) * kD;    // [X0; Ve]
     U = p;    p += kT * kD;          // Bv @ Wi
     E = p;    p += kT * kD;
     C = p;    p += kT * kT;          // cost
     M = p;    p += kL2 * kT;         // Wc @ cost
-    dY = p;   p += kL2 * Nmax;
+    dY = p;   p += kL2 * (Nmax + 1);
     dM = p;   p += kL2 * kT;
     dC = p;   p += kT * kT;
     dE = p;   p += kT * kD;
@@ -2424,6 +2429,21 @@ struct GradArgs {
   int ngroup;
 };
 
+// sum_{i < n} x[i] * y[i * ys] with four independent accumulators (the LDS
+// loads of four terms are in flight together)
+__device__ __forceinline__ float dot_strided(const float* x, const float* y, int ys, int n) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    a0 = fmaf(x[i], y[i * ys], a0);
+    a1 = fmaf(x[i + 1], y[(i + 1) * ys], a1);
+    a2 = fmaf(x[i + 2], y[(i + 2) * ys], a2);
+    a3 = fmaf(x[i + 3], y[(i + 3) * ys], a3);
+  }
+  for (; i < n; ++i) a0 = fmaf(x[i], y[i * ys], a0);
+  return (a0 + a1) + (a2 + a3);
+}
+
 template <int GW>
 __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
   constexpr int NT = 64 * GW;
@@ -2431,13 +2451,11 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
   const int Nmax = a.d.Nmax, F = a.d.F, P = grad_params(Nmax);
   const int s = blockIdx.y, grp = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
-  const int nact = clampi(a.n_active[s], 0, Nmax);
-  const int nf = a.n_frames ? clampi(a.n_frames[s], 0, F) : F;
   const int f = grp * GW + wv;
-  const bool act = f < nf;
   float* sWi = smem;
   float* sWo = sWi + Nmax * kD;
-  float* sWii = sWo + kT * Nmax;
+  const int NP1 = Nmax + 1;
+  float* sWii = sWo + kT * NP1;
   float* sWv = sWii + kD * kT;
   float* sbv = sWv + kT * (kD + 2);
   float* sWc = sbv + kD;
@@ -2448,33 +2466,40 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
   const GradScratch w(scratch0 + wv * PW, Nmax);
   const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
 
-  for (int i = tid; i < Nmax * kD; i += NT) sWi[i] = a.w.Wi[i];
-  for (int i = tid; i < kT * Nmax; i += NT) sWo[i] = a.w.Wo[i];
-  for (int i = tid; i < kD * kT; i += NT) {
-    sWii[i] = a.w.Wii[i];
-    sg[i] = a.lambda * a.G[(size_t)s * kD * kT + i];
+  // every global byte by 4-byte LDS-DMA, all in flight before n_active /
+  // n_frames are known and before any use (one vmcnt wait): weights, G and
+  // vislet per workgroup; each wave its frame's position window and targets
+  dma4_copy_t<NT>(a.w.Wi, sWi, Nmax * kD, wv, lane);
+  for (int t = 0; t < kT; ++t) dma4_copy_t<NT>(a.w.Wo + t * Nmax, sWo + t * NP1, Nmax, wv, lane);
+  dma4_copy_t<NT>(a.w.Wii, sWii, kD * kT, wv, lane);
+  dma4_copy_t<NT>(a.w.Wv, sWv, kT * (kD + 2), wv, lane);
+  dma4_copy_t<NT>(a.w.bv, sbv, kD, wv, lane);
+  dma4_copy_t<NT>(a.w.Wc, sWc, kL2 * kT, wv, lane);
+  dma4_copy_t<NT>(a.G + (size_t)s * kD * kT, sg, kD * kT, wv, lane);   // lambda applied at use
+  for (int j = 0; j < 2; ++j)
+    dma4_copy_t<NT>(a.vislet + ((size_t)s * 2 + j) * Nmax, sVis + j * NP1, Nmax, wv, lane);
+  if (f < F) {
+    for (int t = 0; t < kT; ++t)
+      dma4_copy_t<64>(a.pos + ((size_t)s * a.d.W + (size_t)f * a.d.stride + t) * Nmax * 2,
+                      w.pos + t * 2 * Nmax, 2 * Nmax, 0, lane);
+    dma4_copy_t<64>(a.targets + ((size_t)s * F + f) * Nmax * kL2, w.tgt, kL2 * Nmax, 0, lane);
   }
-  for (int i = tid; i < kT * (kD + 2); i += NT) sWv[i] = a.w.Wv[i];
-  for (int i = tid; i < kL2 * kT; i += NT) sWc[i] = a.w.Wc[i];
-  if (tid < kD) sbv[tid] = a.w.bv[tid];
-  for (int i = tid; i < 2 * Nmax; i += NT) sVis[i] = a.vislet[(size_t)s * 2 * Nmax + i];
+  const int nact = clampi(a.n_active[s], 0, Nmax);
+  const int nf = a.n_frames ? clampi(a.n_frames[s], 0, F) : F;
+  const bool act = f < nf;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int i = lane; i < kT * Nmax; i += 64) {                 // a2 window norms (train.py:76-85)
     const int t = i / Nmax, n = i - t * Nmax;
-    float v = 0.f;
-    if (act && n < nact) {
-      const float2 p = *reinterpret_cast<const float2*>(
-          a.pos + (((size_t)s * a.d.W + (size_t)f * a.d.stride + t) * Nmax + n) * 2);
-      v = sqrtf(fmaf(p.x, p.x, p.y * p.y));
-    }
-    w.B[i] = v;
+    const float2 p = *reinterpret_cast<const float2*>(w.pos + t * 2 * Nmax + 2 * n);
+    w.B[t * NP1 + n] = (act && n < nact) ? sqrtf(fmaf(p.x, p.x, p.y * p.y)) : 0.f;
   }
   __syncthreads();
   // forward (train.py:178-195, models/g2k_lstm_mcr.py:105-122)
   for (int o = lane; o < (kT + 2) * kD; o += 64) {           // U = Bv @ Wi; Ve = vislet @ Wi
     const int r = o >> 4, d = o & 15;
-    const float* src = r < kT ? w.B + r * Nmax : sVis + (r - kT) * Nmax;
-    float acc = 0.f;
-    for (int n = 0; n < nact; ++n) acc = fmaf(src[n], sWi[n * kD + d], acc);
+    const float* src = r < kT ? w.B + r * NP1 : sVis + (r - kT) * NP1;
+    const float acc = dot_strided(src, sWi + d, kD, nact);
     if (r < kT) w.U[r * kD + d] = acc;
     else w.X[(kD + r - kT) * kD + d] = acc;
   }
@@ -2500,7 +2525,7 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     float acc = 0.f;
 #pragma unroll
     for (int d = 0; d < kD; ++d) acc = fmaf(w.E[t * kD + d], sg[d * kT + u], acc);
-    w.C[lane] = acc;
+    w.C[lane] = a.lambda * acc;
   }
   __syncthreads();
   for (int o = lane; o < kL2 * kT; o += 64) {                 // M = Wc @ cost
@@ -2513,18 +2538,19 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
   __syncthreads();
   // dY = Y - target on active, masked pedestrians (Y = M @ Wo, :122-124)
   float lsum = 0.f;
-  for (int o = lane; o < kL2 * Nmax; o += 64) {
-    const int r = o / Nmax, n = o - r * Nmax;
+  for (int o = lane; o < kL2 * Nmax; o += 64) {     // o walks targets[n][l][x|y]
+    const int n = o / kL2, rem = o - n * kL2, l = rem >> 1;
+    const int r = (rem & 1) ? kL + l : l;
     float dy = 0.f;
     if (act && n < nact && (pm ? pm[n] != 0 : true)) {
+      const float tg = w.tgt[o];
       float y = 0.f;
 #pragma unroll
-      for (int t = 0; t < kT; ++t) y = fmaf(w.M[r * kT + t], sWo[t * Nmax + n], y);
-      const int l = r < kL ? r : r - kL;
-      dy = y - a.targets[((((size_t)s * F + f) * Nmax + n) * kL + l) * 2 + (r < kL ? 0 : 1)];
+      for (int t = 0; t < kT; ++t) y = fmaf(w.M[r * kT + t], sWo[t * NP1 + n], y);
+      dy = y - tg;
       lsum = fmaf(dy, dy, lsum);
     }
-    w.dY[o] = dy;
+    w.dY[r * NP1 + n] = dy;
   }
   float cnt = 0.f;
   for (int n = lane; n < Nmax; n += 64) cnt += (act && n < nact && (pm ? pm[n] != 0 : true)) ? 1.f : 0.f;
@@ -2538,9 +2564,7 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
   // backward
   for (int o = lane; o < kL2 * kT; o += 64) {                 // dM = dY @ Wo^T
     const int r = o >> 3, t = o & 7;
-    float acc = 0.f;
-    for (int n = 0; n < nact; ++n) acc = fmaf(w.dY[r * Nmax + n], sWo[t * Nmax + n], acc);
-    w.dM[o] = acc;
+    w.dM[o] = dot_strided(w.dY + r * NP1, sWo + t * NP1, 1, nact);
   }
   __syncthreads();
   for (int o = lane; o < kT * kT + kL2 * kT; o += 64) {
@@ -2563,7 +2587,7 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     float acc = 0.f;
 #pragma unroll
     for (int u = 0; u < kT; ++u) acc = fmaf(w.dC[t * kT + u], sg[d * kT + u], acc);
-    w.dE[o] = acc;
+    w.dE[o] = a.lambda * acc;
   }
   __syncthreads();
   for (int o = lane; o < (kD + 2) * kD + kT * (kD + 2) + kD; o += 64) {
@@ -2616,9 +2640,9 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
         const int n = p >> 4, d = p & 15;
         if (n < nact) {
 #pragma unroll
-          for (int t = 0; t < kT; ++t) c = fmaf(x.B[t * Nmax + n], x.dU[t * kD + d], c);
+          for (int t = 0; t < kT; ++t) c = fmaf(x.B[t * NP1 + n], x.dU[t * kD + d], c);
           c = fmaf(sVis[n], x.dX[kD * kD + d], c);
-          c = fmaf(sVis[Nmax + n], x.dX[(kD + 1) * kD + d], c);
+          c = fmaf(sVis[NP1 + n], x.dX[(kD + 1) * kD + d], c);
         }
       } else if (p < go.wv) {
         c = x.gWii[p - go.wii];
@@ -2632,7 +2656,7 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
         c = x.gWc[p - go.wc];
       } else if (p < P) {                                     // dWo = M^T @ dY
         const int q = p - go.wo, t = q / Nmax, n = q - t * Nmax;
-        for (int r = 0; r < kL2; ++r) c = fmaf(x.M[r * kT + t], x.dY[r * Nmax + n], c);
+        for (int r = 0; r < kL2; ++r) c = fmaf(x.M[r * kT + t], x.dY[r * NP1 + n], c);
       } else {
         c = x.loss[p - P];
       }
@@ -3120,10 +3144,13 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
   a.n_active = n_active; a.n_frames = n_frames; a.ped_mask = ped_mask; a.lambda = lambda;
   a.part = static_cast<float*>(workspace); a.ngroup = ngroup;
   float* red = a.part + (size_t)d->S * ngroup * width;
+  const dim3 grid(ngroup, d->S);
   if (GW == 4)
-    hipLaunchKernelGGL((g2k_grad_kernel<4>), dim3(ngroup, d->S), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((g2k_grad_kernel<4>), grid, dim3(256), lds, st, a);
+  else if (GW == 2)
+    hipLaunchKernelGGL((g2k_grad_kernel<2>), grid, dim3(128), lds, st, a);
   else
-    hipLaunchKernelGGL((g2k_grad_kernel<2>), dim3(ngroup, d->S), dim3(128), lds, st, a);
+    hipLaunchKernelGGL((g2k_grad_kernel<1>), grid, dim3(64), lds, st, a);
   if ((rc = check_launch("g2k_step_grad_f32/grad"))) return rc;
   const unsigned gx = (unsigned)((width + 255) / 256);
   hipLaunchKernelGGL(g2k_grad_reduce1_kernel, dim3(gx, kGradSlices), dim3(256), 0, st, a.part, red,
