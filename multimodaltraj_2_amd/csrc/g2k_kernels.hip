@@ -1,21 +1,17 @@
 // g2k_kernels.hip — gfx950 (CDNA4) kernels + C ABI for the g2k_lstm_mcr
-// per-frame path of serenetech90/multimodaltraj_2 (SURVEY.md §8).
+// per-frame path of serenetech90/multimodaltraj_2 (SURVEY.md §8; DESIGN.md §6).
 //
-// The step (train.py:197-276 over S scenes x F frames) is two launches on one
-// stream:
-//   1. g2k_frames_kernel — frame-parallel part (a2-a7, a9): grid =
-//      (frame chunks) x S, 256 threads.  The chunk's targets arrive in LDS by
-//      LDS-DMA (global_load_lds_dwordx4) while the window norms, embeddings,
-//      g2k_lstm_mcr forward (X0, E, A, cost, Wc@cost) run as batched tiny
-//      matmuls out of LDS; predictions are stored, ADE/FDE partial sums and
-//      the attention weights As = softmax(exp(A)/cumsum(exp(A))) go to a
-//      workspace.  Many small workgroups per CU hide the latency chains.
-//   2. g2k_recur_kernel — frame-sequential part (a8): one workgroup per
-//      scene keeps h [16, H] in registers in the v_mfma_f32_16x16x4_f32 C
-//      layout; per frame: one MFMA contraction, one row-softmax reduction
-//      (16-lane DPP + ONE 4-wave LDS exchange), no global traffic except the
-//      LDS-DMA of the scene's As tiles.
-// Deterministic: fixed reduction order, no atomics.
+//   g2k_scene_kernel — the step (train.py:197-276 over S scenes x F frames) in
+//      ONE launch: one workgroup per scene; producer waves run the frame heads
+//      (a2-a7), predictions and a9 errors per frame, recurrence waves run a8
+//      with h [16, H] in MFMA registers; LDS flags between them, barriers
+//      only at chunk boundaries.
+//   g2k_frames_kernel + g2k_recur_kernel — the earlier two-kernel split
+//      (G2K_STEP_SPLIT=1, g2k_frame_recurrence_f32).
+//   g2k_mcr_forward_kernel, g2k_errors_v0/v1_kernel, relation ops (a7, a9, a11).
+//   g2k_gridlstm_kernel — GridLSTMCell encoders (a6).
+//   g2k_grad_kernel + reductions + g2k_update_kernel — train mode.
+// Deterministic: fixed reduction order, no float atomics.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
