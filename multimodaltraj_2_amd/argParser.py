@@ -37,3 +37,5 @@ class ArgsParser:
                         help='carry hidden_state from batch to batch like train.py')
     parser.add_argument('--log_dir', type=str, default='log')
     parser.add_argument('--seed', type=int, default=0)
+    parser.add_argument('--save_dir', type=str, default='',
+                        help='write TF-bundle checkpoints every --save_every batches (train.py:330-343)')

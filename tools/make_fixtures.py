@@ -30,7 +30,6 @@ from __future__ import annotations
 
 import glob
 import os
-import struct
 import sys
 
 import numpy as np
@@ -128,70 +127,9 @@ def make_data_fixture(name, rel):
     return rec
 
 
-# ---------------------------------------------------------------------------
-# TF tensor bundle (.index = LevelDB-style table of BundleEntryProto)
-# ---------------------------------------------------------------------------
-def _varint(b, i):
-    r = s = 0
-    while True:
-        c = b[i]; i += 1
-        r |= (c & 0x7F) << s; s += 7
-        if c < 0x80:
-            return r, i
-
-
-def _block_entries(buf):
-    nrest = struct.unpack_from("<I", buf, len(buf) - 4)[0]
-    end = len(buf) - 4 - 4 * nrest
-    i, key, out = 0, b"", []
-    while i < end:
-        shared, i = _varint(buf, i)
-        nonshared, i = _varint(buf, i)
-        vlen, i = _varint(buf, i)
-        key = key[:shared] + buf[i:i + nonshared]; i += nonshared
-        out.append((key, buf[i:i + vlen])); i += vlen
-    return out
-
-
-def _proto_fields(b):
-    i, out = 0, {}
-    while i < len(b):
-        tag, i = _varint(b, i)
-        f, wt = tag >> 3, tag & 7
-        if wt == 0:
-            v, i = _varint(b, i)
-        elif wt == 2:
-            n, i = _varint(b, i); v = b[i:i + n]; i += n
-        elif wt == 5:
-            v = b[i:i + 4]; i += 4
-        elif wt == 1:
-            v = b[i:i + 8]; i += 8
-        else:
-            raise ValueError("wire type")
-        out.setdefault(f, []).append(v)
-    return out
-
-
-def read_bundle(prefix):
-    idx = open(prefix + ".index", "rb").read()
-    data = open(prefix + ".data-00000-of-00001", "rb").read()
-    footer = idx[-48:]
-    _, j = _varint(footer, 0); _, j = _varint(footer, j)      # metaindex handle
-    ioff, j = _varint(footer, j); isz, j = _varint(footer, j)  # index handle
-    tensors = {}
-    for _, handle in _block_entries(idx[ioff:ioff + isz]):
-        off, k = _varint(handle, 0); sz, k = _varint(handle, k)
-        for key, val in _block_entries(idx[off:off + sz]):
-            if not key:
-                continue                               # header entry
-            fl = _proto_fields(val)
-            dtype = fl.get(1, [0])[0]
-            shape = [_proto_fields(d).get(1, [0])[0]
-                     for d in _proto_fields(fl[2][0]).get(2, [])] if 2 in fl else []
-            o = fl.get(4, [0])[0]; n = fl.get(5, [0])[0]
-            if dtype == 2:                             # DT_DOUBLE
-                tensors[key.decode()] = np.frombuffer(data[o:o + n], dtype="<f8").reshape(shape)
-    return tensors
+# TF tensor bundle reader: the package's (multimodaltraj_2_amd/checkpoint.py)
+sys.path.insert(0, ROOT)
+from multimodaltraj_2_amd.checkpoint import read_bundle  # noqa: E402
 
 
 def make_ckpt_fixture():
