@@ -221,6 +221,21 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
 int g2k_update_f32(float* params, float* ms, const float* grad, int64_t n_params, float lr,
                    float decay, float grad_clip, void* stream);
 
+/*
+ * g2k_context_conv_f32 — the static-context input (a5).
+ * Replaces: train.py:92-113 (_2dconv = lambda * squeeze(conv2d(pad(img,
+ * [[1,1],[0,1],[0,0]]), filter [H+3-D, W+2-D, C, 1], VALID))) and
+ * train.py:154-158 (_2dconv_in = _2dconv @ stat_mask, stat_mask [D, T] rows
+ * (0, 1/T, ..., (T-1)/T)).
+ *   img  [Hh, Ww, C] (HWC, C <= 4)     filt [Hh+3-D, Ww+2-D, C]
+ *   out  [D, D] or NULL                 G [D, T = 8] or NULL (one must be set)
+ *   D in 1..16; workspace >= g2k_context_conv_workspace_bytes(Hh, Ww, D).
+ */
+int64_t g2k_context_conv_workspace_bytes(int32_t Hh, int32_t Ww, int32_t D);
+int g2k_context_conv_f32(const float* img, int32_t Hh, int32_t Ww, int32_t C, const float* filt,
+                         int32_t D, float lambda, float* out, float* G, void* workspace,
+                         int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,7 @@
 //   g2k_mcr_forward_kernel, g2k_errors_v0/v1_kernel, relation ops (a7, a9, a11).
 //   g2k_gridlstm_kernel — GridLSTMCell encoders (a6).
 //   g2k_grad_kernel + reductions + g2k_update_kernel — train mode.
+//   g2k_ctx_conv_kernel + g2k_ctx_reduce_kernel — static-context input (a5).
 // Deterministic: fixed reduction order, no float atomics.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
@@ -2723,6 +2724,87 @@ __global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ pa
 }
 
 // ---------------------------------------------------------------------------
+// a5 static-context input (train.py:92-113, 154-158):
+//   _2dconv = lambda * conv2d_VALID(pad(img, [[1,1],[0,1],[0,0]]), K)  [D, D]
+//   G       = _2dconv @ stat_mask,  stat_mask[j][t] = t / T           [D, T]
+// (tf.nn.conv2d is a cross-correlation; K is the reference's
+// [H+3-D, W+2-D, C, 1] filter, so the VALID output is D x D.)  One-off work
+// (~3e8 MACs for a 576x720 image): g2k_ctx_conv_kernel takes one filter row
+// a per workgroup, stages it and the D padded image rows it meets in LDS and
+// forms every output's partial over that row; g2k_ctx_reduce_kernel sums the
+// partials over a in a fixed order (deterministic) and forms G.
+// ---------------------------------------------------------------------------
+struct CtxArgs {
+  const float* img;
+  const float* filt;
+  float* part;      // [KH][D * D]
+  float* out;       // [D, D] or NULL
+  float* G;         // [D, T] or NULL
+  int Hh, Ww, C, D, KH, KW;
+  float lambda;
+};
+
+__global__ void __launch_bounds__(256) g2k_ctx_conv_kernel(CtxArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int C = a.C, D = a.D, KW = a.KW, pitch = (a.Ww + 1) * C;   // padded row: Ww + 1 columns
+  float* sK = smem;                                                // filter row `row` [KW][C]
+  float* sI = smem + ((KW * C + 3) & ~3);                          // padded rows row .. row+D-1
+  for (int i = tid; i < KW * C; i += 256) sK[i] = a.filt[(size_t)row * KW * C + i];
+  for (int i = tid; i < D * pitch; i += 256) {
+    const int r = i / pitch, x = i - r * pitch;
+    const int pr = row + r;                                        // padded row index
+    const bool in = pr >= 1 && pr <= a.Hh && x < a.Ww * C;
+    sI[i] = in ? a.img[(size_t)(pr - 1) * a.Ww * C + x] : 0.f;
+  }
+  __syncthreads();
+  if (tid < D * D) {
+    const int i = tid / D, j = tid - (tid / D) * D;
+    const float* src = sI + i * pitch + j * C;
+    const int n = KW * C;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int k = 0;
+    for (; k + 4 <= n; k += 4) {
+      a0 = fmaf(src[k], sK[k], a0);
+      a1 = fmaf(src[k + 1], sK[k + 1], a1);
+      a2 = fmaf(src[k + 2], sK[k + 2], a2);
+      a3 = fmaf(src[k + 3], sK[k + 3], a3);
+    }
+    for (; k < n; ++k) a0 = fmaf(src[k], sK[k], a0);
+    a.part[(size_t)row * D * D + tid] = (a0 + a1) + (a2 + a3);
+  }
+}
+
+// one workgroup per output row i: slice s of 256 / D threads sums filter rows
+// a = s, s + slices, ... for column j; then the slices in order, lambda, G
+__global__ void __launch_bounds__(256) g2k_ctx_reduce_kernel(CtxArgs a) {
+  __shared__ float red[256];
+  __shared__ float rowv[32];
+  const int i = blockIdx.x, tid = threadIdx.x, D = a.D;
+  const int slices = 256 / D, j = tid % D, sl = tid / D;
+  float acc = 0.f;
+  if (sl < slices) {
+#pragma unroll 4
+    for (int r = sl; r < a.KH; r += slices) acc += a.part[(size_t)r * D * D + i * D + j];
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (tid < D) {
+    float v = 0.f;
+    for (int s = 0; s < slices; ++s) v += red[s * D + tid];
+    v *= a.lambda;
+    rowv[tid] = v;
+    if (a.out) a.out[i * D + tid] = v;
+  }
+  __syncthreads();
+  if (a.G && tid < kT) {
+    float rs = 0.f;
+    for (int q = 0; q < D; ++q) rs += rowv[q];
+    a.G[i * kT + tid] = rs * ((float)tid / (float)kT);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host-side validation / geometry
 // ---------------------------------------------------------------------------
 int validate_common(const g2k_dims* d, bool need_F) {
@@ -3163,6 +3245,31 @@ int g2k_update_f32(float* params, float* ms, const float* grad, int64_t n_params
   hipLaunchKernelGGL(g2k_update_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, params, ms, grad,
                      (int)n_params, lr, decay, grad_clip);
   return check_launch("g2k_update_f32");
+}
+
+int64_t g2k_context_conv_workspace_bytes(int32_t Hh, int32_t Ww, int32_t D) {
+  if (Hh < 1 || Ww < 1 || D < 1 || D > 16 || Hh + 3 - D < 1 || Ww + 2 - D < 1) return -1;
+  return (int64_t)(Hh + 3 - D) * D * D * 4;
+}
+
+int g2k_context_conv_f32(const float* img, int32_t Hh, int32_t Ww, int32_t C, const float* filt,
+                         int32_t D, float lambda, float* out, float* G, void* workspace,
+                         int64_t workspace_bytes, void* stream) {
+  if (!img || !filt || (!out && !G)) return set_err(G2K_EINVAL, "a required buffer pointer is NULL");
+  if (C < 1 || C > 4) return set_err(G2K_EUNSUPPORTED, "C=%d channels (1..4)", C);
+  const int64_t need = g2k_context_conv_workspace_bytes(Hh, Ww, D);
+  if (need < 0) return set_err(G2K_EINVAL, "image %dx%d, D=%d (D in 1..16, image >= D)", Hh, Ww, D);
+  if (!workspace || workspace_bytes < need)
+    return set_err(G2K_EINVAL, "workspace of %lld bytes needed", (long long)need);
+  CtxArgs a;
+  a.img = img; a.filt = filt; a.part = static_cast<float*>(workspace); a.out = out; a.G = G;
+  a.Hh = Hh; a.Ww = Ww; a.C = C; a.D = D; a.KH = Hh + 3 - D; a.KW = Ww + 2 - D; a.lambda = lambda;
+  const size_t lds = (size_t)4 * (((a.KW * C + 3) & ~3) + (size_t)D * (Ww + 1) * C);
+  if (lds > 160 * 1024) return set_err(G2K_ELDS, "image width %d needs %zu bytes of LDS", Ww, lds);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(g2k_ctx_conv_kernel, dim3(a.KH), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(g2k_ctx_reduce_kernel, dim3(D), dim3(256), 0, st, a);
+  return check_launch("g2k_context_conv_f32");
 }
 
 }  // extern "C"

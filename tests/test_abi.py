@@ -105,3 +105,13 @@ def test_gridlstm_and_train_entry_points_validate():
     assert rc == -4
     assert lib.g2k_update_f32(None, None, p, 10, 0.1, 0.9, 10.0, None) == -1
     assert lib.g2k_update_f32(p, None, p, 0, 0.1, 0.9, 10.0, None) == 0
+
+
+def test_context_conv_validates():
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)
+    assert lib.g2k_context_conv_workspace_bytes(576, 720, 16) == (576 + 3 - 16) * 256 * 4
+    assert lib.g2k_context_conv_workspace_bytes(10, 10, 16) == -1
+    assert lib.g2k_context_conv_f32(p, 576, 720, 5, p, 16, 5e-4, p, None, p, 1 << 30, None) == -4
+    assert lib.g2k_context_conv_f32(p, 576, 720, 3, p, 16, 5e-4, None, None, p, 1 << 30, None) == -1
+    assert lib.g2k_context_conv_f32(p, 576, 720, 3, p, 16, 5e-4, p, None, p, 16, None) == -1
