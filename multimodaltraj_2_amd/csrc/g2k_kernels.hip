@@ -2874,11 +2874,15 @@ int launch_recur(const RecurArgs& r, int S, hipStream_t st) {
   return G2K_OK;
 }
 
-// Fused scene kernel geometry: producer waves (NP) and the frames-per-chunk
-// that fits LDS.  NP = 8 by default (12 waves: one recurrence + two producer
-// waves per SIMD); G2K_SCENE_NP in {4, 6, 8, 12} is a tuning override.
-int scene_producers(int H) {
-  int np = 8;
+// Fused scene kernel geometry: producer waves (NP).  Measured (gpurun_out
+// d38, 400 steps): eth_hotel_synth (H 128, Nmax 32) NP 8 19.9 us vs NP 12
+// 20.2, NP 6 22.2, NP 4 24.3; H 256 / Nmax 64: NP 12 28.2 vs NP 8 29.6;
+// dense crowd (H 256, Nmax 256): NP 12 53.2 vs NP 8 60.5; k-fold (H 128,
+// Nmax 64, d39): NP 12 23.6 vs NP 8 25.4.  So 12 producers (16 waves, 4 per
+// SIMD) once H >= 256 or Nmax >= 64, else 8.
+// G2K_SCENE_NP in {4, 6, 8, 12} is a tuning override.
+int scene_producers(int H, int Nmax) {
+  int np = (H >= 256 || Nmax >= 64) ? 12 : 8;
   const char* env = getenv("G2K_SCENE_NP");
   if (env && (atoi(env) == 4 || atoi(env) == 6 || atoi(env) == 8 || atoi(env) == 12)) np = atoi(env);
   if (H >= 512) np = 4;            // TPW 8 needs > 128 VGPRs: at most 512 threads
@@ -3042,7 +3046,7 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
   a.ws_part = a.ws_as + (size_t)d->S * d->F * kD * kD;
   hipStream_t st = (hipStream_t)stream;
   if (!use_split_step()) {
-    const int NP = scene_producers(d->H);
+    const int NP = scene_producers(d->H, d->Nmax);
     const SceneLayout l = scene_layout(d, NP);
     if ((int64_t)l.total * 4 > 160 * 1024)
       return set_err(G2K_ELDS, "Nmax=%d, stride=%d needs %lld bytes of LDS", d->Nmax, d->stride,
