@@ -2381,27 +2381,25 @@ __host__ __device__ inline GradOff grad_off(int Nmax) {   // g2k_weights order
   return o;
 }
 
-// rows that lanes walk in parallel (window norms, dY, Wo, vislet) have the
+// rows that lanes walk in parallel (window norms, Wo, vislet) have the
 // odd pitch Nmax + 1, so lanes on different rows hit different LDS banks
 __host__ __device__ inline int grad_shared_floats(int Nmax) { return 26 * Nmax + 618; }
-__host__ __device__ inline int grad_scratch_floats(int Nmax) { return 72 * Nmax + 2116; }
-__host__ __device__ inline int grad_waves(int Nmax) { return Nmax > 128 ? 1 : (Nmax > 64 ? 2 : 4); }
+__host__ __device__ inline int grad_scratch_floats(int Nmax) { return 48 * Nmax + 2092; }
+__host__ __device__ inline int grad_waves(int Nmax) { return Nmax > 128 ? 2 : 4; }
 constexpr int kGradSlices = 32;
 
 // one wave's LDS scratch in g2k_grad_kernel (floats)
 struct GradScratch {
-  float *pos, *tgt, *B, *X, *U, *E, *C, *M, *dY, *dM, *dC, *dE, *dX, *dU, *gWc, *gWv, *gbv, *gWii,
-      *loss;
+  float *pos, *tgt, *B, *X, *U, *E, *C, *M, *dM, *dC, *dE, *dX, *dU, *gWc, *gWv, *gbv, *gWii, *loss;
   __device__ GradScratch(float* p, int Nmax) {
     pos = p;  p += kT * 2 * Nmax;    // the frame's raw position window (LDS-DMA)
-    tgt = p;  p += kL2 * Nmax;       // the frame's targets [Nmax][L][2] (LDS-DMA)
+    tgt = p;  p += kL2 * Nmax;       // the frame's targets [Nmax][L][2] (LDS-DMA), then dY in place
     B = p;    p += kT * (Nmax + 1);  // window norms [T][Nmax + 1] (a2)
     X = p;    p += (kD + 2) * kD;    // [X0; Ve]
     U = p;    p += kT * kD;          // Bv @ Wi
     E = p;    p += kT * kD;
     C = p;    p += kT * kT;          // cost
     M = p;    p += kL2 * kT;         // Wc @ cost
-    dY = p;   p += kL2 * (Nmax + 1);
     dM = p;   p += kL2 * kT;
     dC = p;   p += kT * kT;
     dE = p;   p += kT * kD;
@@ -2547,7 +2545,7 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
       dy = y - tg;
       lsum = fmaf(dy, dy, lsum);
     }
-    w.dY[r * NP1 + n] = dy;
+    w.tgt[o] = dy;                                    // dY(r, n), in place
   }
   float cnt = 0.f;
   for (int n = lane; n < Nmax; n += 64) cnt += (act && n < nact && (pm ? pm[n] != 0 : true)) ? 1.f : 0.f;
@@ -2561,7 +2559,16 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
   // backward
   for (int o = lane; o < kL2 * kT; o += 64) {                 // dM = dY @ Wo^T
     const int r = o >> 3, t = o & 7;
-    w.dM[o] = dot_strided(w.dY + r * NP1, sWo + t * NP1, 1, nact);
+    const float* dy = w.tgt + ((r < kL) ? 2 * r : 2 * (r - kL) + 1);   // dY(r, n) at dy[24 n]
+    const float* wo = sWo + t * NP1;
+    float a0 = 0.f, a1 = 0.f;
+    int n = 0;
+    for (; n + 2 <= nact; n += 2) {
+      a0 = fmaf(dy[n * kL2], wo[n], a0);
+      a1 = fmaf(dy[(n + 1) * kL2], wo[n + 1], a1);
+    }
+    if (n < nact) a0 = fmaf(dy[n * kL2], wo[n], a0);
+    w.dM[o] = a0 + a1;
   }
   __syncthreads();
   for (int o = lane; o < kT * kT + kL2 * kT; o += 64) {
@@ -2653,7 +2660,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
         c = x.gWc[p - go.wc];
       } else if (p < P) {                                     // dWo = M^T @ dY
         const int q = p - go.wo, t = q / Nmax, n = q - t * Nmax;
-        for (int r = 0; r < kL2; ++r) c = fmaf(x.M[r * kT + t], x.dY[r * NP1 + n], c);
+        for (int r = 0; r < kL2; ++r)
+          c = fmaf(x.M[r * kT + t], x.tgt[n * kL2 + ((r < kL) ? 2 * r : 2 * (r - kL) + 1)], c);
       } else {
         c = x.loss[p - P];
       }
