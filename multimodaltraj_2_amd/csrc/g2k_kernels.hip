@@ -2386,6 +2386,15 @@ __host__ __device__ inline GradOff grad_off(int Nmax) {   // g2k_weights order
 __host__ __device__ inline int grad_shared_floats(int Nmax) { return 26 * Nmax + 618; }
 __host__ __device__ inline int grad_scratch_floats(int Nmax) { return 48 * Nmax + 2092; }
 __host__ __device__ inline int grad_waves(int Nmax) { return Nmax > 128 ? 2 : 4; }
+// launch width: grad_waves, or the G2K_GRAD_GW tuning override (1, 2, 4)
+inline int grad_gw(int Nmax) {
+  int GW = grad_waves(Nmax);
+  if (const char* e = getenv("G2K_GRAD_GW")) {
+    const int g = atoi(e);
+    if (g == 1 || g == 2 || (g == 4 && Nmax <= 128)) GW = g;
+  }
+  return GW;
+}
 constexpr int kGradSlices = 32;
 
 // one wave's LDS scratch in g2k_grad_kernel (floats)
@@ -2439,6 +2448,14 @@ __device__ __forceinline__ float dot_strided(const float* x, const float* y, int
   return (a0 + a1) + (a2 + a3);
 }
 
+// LDS hand-off between the lanes of ONE wave: DS instructions of a wave
+// complete in issue order, so only compiler reordering has to be fenced
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int GW>
 __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
   constexpr int NT = 64 * GW;
@@ -2447,6 +2464,7 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
   const int s = blockIdx.y, grp = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
   const int f = grp * GW + wv;
+  STAMP(18);
   float* sWi = smem;
   float* sWo = sWi + Nmax * kD;
   const int NP1 = Nmax + 1;
@@ -2484,12 +2502,14 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
   const bool act = f < nf;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  STAMP(19);
   for (int i = lane; i < kT * Nmax; i += 64) {                 // a2 window norms (train.py:76-85)
     const int t = i / Nmax, n = i - t * Nmax;
     const float2 p = *reinterpret_cast<const float2*>(w.pos + t * 2 * Nmax + 2 * n);
     w.B[t * NP1 + n] = (act && n < nact) ? sqrtf(fmaf(p.x, p.x, p.y * p.y)) : 0.f;
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(20);
   // forward (train.py:178-195, models/g2k_lstm_mcr.py:105-122)
   for (int o = lane; o < (kT + 2) * kD; o += 64) {           // U = Bv @ Wi; Ve = vislet @ Wi
     const int r = o >> 4, d = o & 15;
@@ -2498,7 +2518,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     if (r < kT) w.U[r * kD + d] = acc;
     else w.X[(kD + r - kT) * kD + d] = acc;
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(21);
   for (int o = lane; o < kD * kD; o += 64) {                  // X0 = Wii @ U
     const int r = o >> 4, d = o & 15;
     float acc = 0.f;
@@ -2506,7 +2527,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     for (int t = 0; t < kT; ++t) acc = fmaf(sWii[r * kT + t], w.U[t * kD + d], acc);
     w.X[o] = acc;
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(22);
   for (int o = lane; o < kT * kD; o += 64) {                  // E = Wv @ X + bv
     const int t = o >> 4, d = o & 15;
     float acc = sbv[d];
@@ -2514,7 +2536,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     for (int c = 0; c < kD + 2; ++c) acc = fmaf(sWv[t * (kD + 2) + c], w.X[c * kD + d], acc);
     w.E[o] = acc;
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(23);
   {                                                           // cost = E @ (lambda G)
     const int t = lane >> 3, u = lane & 7;
     float acc = 0.f;
@@ -2522,7 +2545,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     for (int d = 0; d < kD; ++d) acc = fmaf(w.E[t * kD + d], sg[d * kT + u], acc);
     w.C[lane] = a.lambda * acc;
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(24);
   for (int o = lane; o < kL2 * kT; o += 64) {                 // M = Wc @ cost
     const int r = o >> 3, t = o & 7;
     float acc = 0.f;
@@ -2530,7 +2554,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     for (int u = 0; u < kT; ++u) acc = fmaf(sWc[r * kT + u], w.C[u * kT + t], acc);
     w.M[o] = acc;
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(25);
   // dY = Y - target on active, masked pedestrians (Y = M @ Wo, :122-124)
   float lsum = 0.f;
   for (int o = lane; o < kL2 * Nmax; o += 64) {     // o walks targets[n][l][x|y]
@@ -2555,7 +2580,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     w.loss[0] = 0.5f * lsum;
     w.loss[1] = cnt;
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(26);
   // backward
   for (int o = lane; o < kL2 * kT; o += 64) {                 // dM = dY @ Wo^T
     const int r = o >> 3, t = o & 7;
@@ -2570,7 +2596,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     if (n < nact) a0 = fmaf(dy[n * kL2], wo[n], a0);
     w.dM[o] = a0 + a1;
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(27);
   for (int o = lane; o < kT * kT + kL2 * kT; o += 64) {
     if (o < kT * kT) {                                        // dcost = Wc^T @ dM
       const int u = o >> 3, t = o & 7;
@@ -2585,7 +2612,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
       w.gWc[p] = acc;
     }
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(28);
   for (int o = lane; o < kT * kD; o += 64) {                  // dE = dcost @ (lambda G)^T
     const int t = o >> 4, d = o & 15;
     float acc = 0.f;
@@ -2593,7 +2621,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     for (int u = 0; u < kT; ++u) acc = fmaf(w.dC[t * kT + u], sg[d * kT + u], acc);
     w.dE[o] = a.lambda * acc;
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(29);
   for (int o = lane; o < (kD + 2) * kD + kT * (kD + 2) + kD; o += 64) {
     if (o < (kD + 2) * kD) {                                  // dX = Wv^T @ dE
       const int c = o >> 4, d = o & 15;
@@ -2615,7 +2644,8 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
       w.gbv[d] = acc;
     }
   }
-  __syncthreads();
+  wave_lds_sync();   // the wave's own scratch only
+  STAMP(30);
   for (int o = lane; o < 2 * kT * kD; o += 64) {
     if (o < kT * kD) {                                        // dU = Wii^T @ dX0
       const int t = o >> 4, d = o & 15;
@@ -2632,6 +2662,7 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     }
   }
   __syncthreads();
+  STAMP(31);
   // this group's gradient row, frames summed in wave order
   const GradOff go = grad_off(Nmax);
   float* row = a.part + ((size_t)s * a.ngroup + grp) * (size_t)(P + 2);
@@ -2669,6 +2700,348 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
     }
     row[p] = v;
   }
+  STAMP(32);
+}
+
+// g2k_grad_seq_kernel: the same per-frame products, but ONE frame at a time
+// over all 256 threads of the workgroup (four times shorter phases), the
+// group's frames in sequence with the next frame's position window and
+// targets prefetched by LDS-DMA under the current frame's work, and the
+// group's row accumulated in LDS by the thread that owns each entry (frame
+// order: the same sums as g2k_grad_kernel's wave-order sum).  One scratch
+// instead of one per wave: ~31 KB of LDS at Nmax = 32, five workgroups per
+// CU, so every (scene, group) of eth_hotel_synth is resident at once.
+__host__ __device__ inline int grad_seq_buf_floats(int Nmax) { return (2 * kT + kL2) * Nmax; }
+__host__ __device__ inline int grad_seq_lds_floats(int Nmax) {
+  return grad_shared_floats(Nmax) + grad_scratch_floats(Nmax) + 8 + grad_seq_buf_floats(Nmax)
+         + grad_params(Nmax) + 2 + Nmax;
+}
+// frames per workgroup: the workgroups run in ceil(groups / slots) rounds of
+// `fpg` sequential frames each (slots = CUs x resident workgroups per CU, by
+// LDS and by the 5-wave-per-SIMD register bound); minimise rounds x fpg,
+// ties to the larger fpg (fewer prologues and partial rows)
+static int grad_cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+inline int grad_seq_fpg(const g2k_dims* d) {
+  if (const char* e = getenv("G2K_GRAD_FPG")) {              // tuning override
+    const int v = atoi(e);
+    if (v >= 1 && v <= 64) return v;
+  }
+  int per_cu = (160 * 1024) / (4 * grad_seq_lds_floats(d->Nmax));
+  per_cu = per_cu < 1 ? 1 : (per_cu > 5 ? 5 : per_cu);
+  const int64_t slots = (int64_t)grad_cu_count() * per_cu;
+  int best = 1;
+  int64_t best_cost = -1;
+  for (int fpg = 1; fpg <= (d->F < 32 ? d->F : 32); ++fpg) {
+    const int64_t groups = (int64_t)d->S * ((d->F + fpg - 1) / fpg);
+    const int64_t cost = ((groups + slots - 1) / slots) * fpg;
+    if (best_cost < 0 || cost <= best_cost) { best = fpg; best_cost = cost; }
+  }
+  return best;
+}
+
+__global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fpg) {
+  constexpr int NT = 256;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Nmax = a.d.Nmax, F = a.d.F, P = grad_params(Nmax), P2 = P + 2;
+  const int s = blockIdx.y, grp = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+  const int NP1 = Nmax + 1;
+  float* sWi = smem;
+  float* sWo = sWi + Nmax * kD;
+  float* sWii = sWo + kT * NP1;
+  float* sWv = sWii + kD * kT;
+  float* sbv = sWv + kT * (kD + 2);
+  float* sWc = sbv + kD;
+  float* sg = sWc + kL2 * kT;
+  float* sVis = sg + kD * kT;
+  float* scr = smem + grad_shared_floats(Nmax);
+  GradScratch w(scr, Nmax);
+  float* sLoss = scr + grad_scratch_floats(Nmax);     // [4 waves][loss, count]
+  float* buf[2] = {w.pos, sLoss + 8};                 // pos window then targets, per frame
+  float* racc = buf[1] + grad_seq_buf_floats(Nmax);  // [P + 2] this group's row
+  float* sAct = racc + P2;                            // [Nmax] 1 for active, masked pedestrians
+  const int f0 = grp * fpg;
+  const int L16 = lane & 15, q4 = lane >> 4;          // MFMA 16x16x4 lane roles
+  const int ntile = (Nmax + 15) >> 4;                 // 16-pedestrian tiles
+  STAMP(18);
+
+  dma4_copy_t<NT>(a.w.Wi, sWi, Nmax * kD, wv, lane);
+  for (int t = 0; t < kT; ++t) dma4_copy_t<NT>(a.w.Wo + t * Nmax, sWo + t * NP1, Nmax, wv, lane);
+  dma4_copy_t<NT>(a.w.Wii, sWii, kD * kT, wv, lane);
+  dma4_copy_t<NT>(a.w.Wv, sWv, kT * (kD + 2), wv, lane);
+  dma4_copy_t<NT>(a.w.bv, sbv, kD, wv, lane);
+  dma4_copy_t<NT>(a.w.Wc, sWc, kL2 * kT, wv, lane);
+  dma4_copy_t<NT>(a.G + (size_t)s * kD * kT, sg, kD * kT, wv, lane);   // lambda applied at use
+  for (int j = 0; j < 2; ++j)
+    dma4_copy_t<NT>(a.vislet + ((size_t)s * 2 + j) * Nmax, sVis + j * NP1, Nmax, wv, lane);
+  auto dma_frame = [&](int f, float* dst) {
+    for (int t = 0; t < kT; ++t)
+      dma4_copy_t<NT>(a.pos + ((size_t)s * a.d.W + (size_t)f * a.d.stride + t) * Nmax * 2,
+                      dst + t * 2 * Nmax, 2 * Nmax, wv, lane);
+    dma4_copy_t<NT>(a.targets + ((size_t)s * F + f) * Nmax * kL2, dst + kT * 2 * Nmax, kL2 * Nmax,
+                    wv, lane);
+  };
+  if (f0 < F) dma_frame(f0, buf[0]);
+  const int nact = clampi(a.n_active[s], 0, Nmax);
+  const int nf = a.n_frames ? clampi(a.n_frames[s], 0, F) : F;
+  // frames past n_frames contribute exactly zero (their dY is masked)
+  const int nfg = max(0, min(fpg, min(nf, F) - f0));
+  const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
+  for (int n = tid; n < Nmax; n += NT) sAct[n] = (n < nact && (pm ? pm[n] != 0 : true)) ? 1.f : 0.f;
+  for (int p = tid; p < P2; p += NT) racc[p] = 0.f;
+  const GradOff go = grad_off(Nmax);
+
+  for (int k = 0; k < nfg; ++k) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                                  // frame k landed; frame k - 1 done
+    STAMP(19);
+    w.pos = buf[k & 1];
+    w.tgt = w.pos + kT * 2 * Nmax;
+    if (k + 1 < nfg) dma_frame(f0 + k + 1, buf[(k + 1) & 1]);
+    for (int i = tid; i < kT * Nmax; i += NT) {       // a2 window norms (train.py:76-85)
+      const int t = i / Nmax, n = i - t * Nmax;
+      const float2 q = *reinterpret_cast<const float2*>(w.pos + t * 2 * Nmax + 2 * n);
+      w.B[t * NP1 + n] = n < nact ? sqrtf(fmaf(q.x, q.x, q.y * q.y)) : 0.f;
+    }
+    __syncthreads();
+    if (wv == 0) {                                    // U = Bv @ Wi; Ve = vislet @ Wi (MFMA,
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};              // rows r < 10 of one 16 x 16 tile, K = n)
+      const float* arow = L16 < kT ? w.B + L16 * NP1 : sVis + (L16 < kT + 2 ? L16 - kT : 0) * NP1;
+      for (int n0 = 0; n0 < nact; n0 += 4) {
+        const int n = n0 + q4;
+        const bool ok = n < nact;
+        const float av = (ok && L16 < kT + 2) ? arow[n] : 0.f;
+        const float bv = ok ? sWi[n * kD + L16] : 0.f;
+        acc = mfma4(av, bv, acc);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int r = 4 * q4 + v;
+        if (r < kT) w.U[r * kD + L16] = acc[v];
+        else if (r < kT + 2) w.X[(kD + r - kT) * kD + L16] = acc[v];
+      }
+    }
+    __syncthreads();
+    {                                                 // X0 = Wii @ U (256 outputs)
+      const int r = tid >> 4, d = tid & 15;
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < kT; ++t) acc = fmaf(sWii[r * kT + t], w.U[t * kD + d], acc);
+      w.X[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < kT * kD) {                              // E = Wv @ X + bv
+      const int t = tid >> 4, d = tid & 15;
+      float acc = sbv[d];
+#pragma unroll
+      for (int c = 0; c < kD + 2; ++c) acc = fmaf(sWv[t * (kD + 2) + c], w.X[c * kD + d], acc);
+      w.E[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < kT * kT) {                              // cost = E @ (lambda G)
+      const int t = tid >> 3, u = tid & 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < kD; ++d) acc = fmaf(w.E[t * kD + d], sg[d * kT + u], acc);
+      w.C[tid] = a.lambda * acc;
+    }
+    __syncthreads();
+    if (tid < kL2 * kT) {                             // M = Wc @ cost
+      const int r = tid >> 3, t = tid & 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int u = 0; u < kT; ++u) acc = fmaf(sWc[r * kT + u], w.C[u * kT + t], acc);
+      w.M[tid] = acc;
+    }
+    __syncthreads();
+    // dY = Y - target on active, masked pedestrians (Y = M @ Wo, :122-124)
+    float lsum = 0.f, cnt = 0.f;
+    for (int it = wv; it < 2 * ntile; it += 4) {      // Y tiles (MFMA): rows r, 16 pedestrians
+      const int rt = it & 1, n = (it >> 1) * 16 + L16;
+      const int ra = rt * 16 + L16;                   // A row of this lane
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int t = 4 * ks + q4;
+        const float av = ra < kL2 ? w.M[ra * kT + t] : 0.f;
+        const float bv = n < Nmax ? sWo[t * NP1 + n] : 0.f;
+        acc = mfma4(av, bv, acc);
+      }
+      if (n < Nmax) {
+        const bool on = sAct[n] != 0.f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int r = rt * 16 + 4 * q4 + v;
+          if (r < kL2) {
+            const int o = n * kL2 + ((r < kL) ? 2 * r : 2 * (r - kL) + 1);
+            float dy = 0.f;
+            if (on) {
+              dy = acc[v] - w.tgt[o];
+              lsum = fmaf(dy, dy, lsum);
+            }
+            w.tgt[o] = dy;                            // dY(r, n), in place
+          }
+        }
+      }
+    }
+    for (int n = tid; n < Nmax; n += NT) cnt += sAct[n];
+    lsum = wave_sum(lsum);
+    cnt = wave_sum(cnt);
+    if (lane == 0) {
+      sLoss[2 * wv] = 0.5f * lsum;
+      sLoss[2 * wv + 1] = cnt;
+    }
+    __syncthreads();
+    if (wv < 2) {                                     // dM = dY @ Wo^T (MFMA, K = n)
+      const int ra = wv * 16 + L16;
+      const int oa = ra < kL2 ? ((ra < kL) ? 2 * ra : 2 * (ra - kL) + 1) : 0;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int n0 = 0; n0 < nact; n0 += 4) {
+        const int n = n0 + q4;
+        const bool ok = n < nact;
+        const float av = (ok && ra < kL2) ? w.tgt[n * kL2 + oa] : 0.f;
+        const float bv = (ok && L16 < kT) ? sWo[L16 * NP1 + n] : 0.f;
+        acc = mfma4(av, bv, acc);
+      }
+      if (L16 < kT) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int r = wv * 16 + 4 * q4 + v;
+          if (r < kL2) w.dM[r * kT + L16] = acc[v];
+        }
+      }
+    } else {                                          // dWo += M^T @ dY (MFMA, K = r)
+      for (int nt = wv - 2; nt < ntile; nt += 2) {
+        const int n = nt * 16 + L16;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < kL2 / 4; ++ks) {
+          const int r = 4 * ks + q4;
+          const float av = L16 < kT ? w.M[r * kT + L16] : 0.f;
+          const float bv = n < Nmax ? w.tgt[n * kL2 + ((r < kL) ? 2 * r : 2 * (r - kL) + 1)] : 0.f;
+          acc = mfma4(av, bv, acc);
+        }
+        if (q4 < 2 && n < Nmax) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) racc[go.wo + (4 * q4 + v) * Nmax + n] += acc[v];
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < kT * kT) {                              // dcost = Wc^T @ dM
+      const int u = tid >> 3, t = tid & 7;
+      float acc = 0.f;
+      for (int r = 0; r < kL2; ++r) acc = fmaf(sWc[r * kT + u], w.dM[r * kT + t], acc);
+      w.dC[tid] = acc;
+    } else {                                          // dWc = dM @ cost^T (192 outputs)
+      const int p = tid - kT * kT, r = p >> 3, u = p & 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < kT; ++t) acc = fmaf(w.dM[r * kT + t], w.C[u * kT + t], acc);
+      w.gWc[p] = acc;
+    }
+    __syncthreads();
+    if (tid < kT * kD) {                              // dE = dcost @ (lambda G)^T
+      const int t = tid >> 4, d = tid & 15;
+      float acc = 0.f;
+#pragma unroll
+      for (int u = 0; u < kT; ++u) acc = fmaf(w.dC[t * kT + u], sg[d * kT + u], acc);
+      w.dE[tid] = a.lambda * acc;
+    }
+    __syncthreads();
+    for (int o = tid; o < (kD + 2) * kD + kT * (kD + 2) + kD; o += NT) {
+      if (o < (kD + 2) * kD) {                        // dX = Wv^T @ dE
+        const int c = o >> 4, d = o & 15;
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < kT; ++t) acc = fmaf(sWv[t * (kD + 2) + c], w.dE[t * kD + d], acc);
+        w.dX[o] = acc;
+      } else if (o < (kD + 2) * kD + kT * (kD + 2)) { // dWv = dE @ X^T
+        const int p = o - (kD + 2) * kD, t = p / (kD + 2), c = p - t * (kD + 2);
+        float acc = 0.f;
+#pragma unroll
+        for (int d = 0; d < kD; ++d) acc = fmaf(w.dE[t * kD + d], w.X[c * kD + d], acc);
+        w.gWv[p] = acc;
+      } else {                                        // dbv = column sums of dE
+        const int d = o - (kD + 2) * kD - kT * (kD + 2);
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < kT; ++t) acc += w.dE[t * kD + d];
+        w.gbv[d] = acc;
+      }
+    }
+    __syncthreads();
+    if (tid < kT * kD) {                              // dU = Wii^T @ dX0
+      const int t = tid >> 4, d = tid & 15;
+      float acc = 0.f;
+#pragma unroll
+      for (int r = 0; r < kD; ++r) acc = fmaf(sWii[r * kT + t], w.dX[r * kD + d], acc);
+      w.dU[tid] = acc;
+    } else {                                          // dWii = dX0 @ U^T (128 outputs)
+      const int p = tid - kT * kD, r = p >> 3, t = p & 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < kD; ++d) acc = fmaf(w.dX[r * kD + d], w.U[t * kD + d], acc);
+      w.gWii[p] = acc;
+    }
+    __syncthreads();
+    for (int nt = wv; nt < ntile; nt += 4) {          // dWi += [Bv; vislet]^T @ [dU; dVe] (MFMA)
+      const int na = nt * 16 + L16;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const int kk = 4 * ks + q4;                  // 8 window rows, 2 vislet rows, 2 zero
+        float av = 0.f, bv = 0.f;
+        if (kk < kT) {
+          av = na < nact ? w.B[kk * NP1 + na] : 0.f;
+          bv = w.dU[kk * kD + L16];
+        } else if (kk < kT + 2) {
+          av = na < nact ? sVis[(kk - kT) * NP1 + na] : 0.f;
+          bv = w.dX[(kD + kk - kT) * kD + L16];
+        }
+        acc = mfma4(av, bv, acc);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int n = nt * 16 + 4 * q4 + v;
+        if (n < Nmax) racc[go.wi + n * kD + L16] += acc[v];
+      }
+    }
+    for (int p = go.wii + tid; p < P2; p += NT) {     // the rest of this frame's row
+      if (p >= go.wo && p < P) continue;              // dWo: accumulated by the MFMA tiles
+      float c;
+      if (p < go.wv) {
+        c = w.gWii[p - go.wii];
+      } else if (p < go.bv) {
+        c = w.gWv[p - go.wv];
+      } else if (p < go.wr) {
+        c = w.gbv[p - go.bv];
+      } else if (p < go.wc) {
+        c = 0.f;                                      // Wr does not reach pred
+      } else if (p < go.wo) {
+        c = w.gWc[p - go.wc];
+      } else {
+        const int j = p - P;                          // loss, count: waves in order
+        c = ((sLoss[j] + sLoss[2 + j]) + sLoss[4 + j]) + sLoss[6 + j];
+      }
+      racc[p] += c;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA outlives the workgroup
+  __syncthreads();
+  float* row = a.part + ((size_t)s * a.ngroup + grp) * (size_t)P2;
+  for (int p = tid; p < P2; p += NT) row[p] = racc[p];
+  STAMP(32);
 }
 
 // pass 1: slice k sums rows k, k + kGradSlices, ... (fixed order)
@@ -3193,10 +3566,26 @@ int64_t g2k_grad_size(const g2k_dims* d) {
   return grad_params(d->Nmax);
 }
 
+// launch shape of the gradient: g2k_grad_seq_kernel with `frames` frames per
+// workgroup (default), or g2k_grad_kernel with one wave per frame when the
+// G2K_GRAD_GW A/B override is set
+struct GradLaunch {
+  bool seq;
+  int frames;   // frames per workgroup
+  int ngroup;
+};
+static GradLaunch grad_launch(const g2k_dims* d) {
+  GradLaunch g;
+  g.seq = getenv("G2K_GRAD_GW") == nullptr &&
+          (size_t)4 * grad_seq_lds_floats(d->Nmax) <= 160 * 1024;
+  g.frames = g.seq ? grad_seq_fpg(d) : grad_gw(d->Nmax);
+  g.ngroup = (d->F + g.frames - 1) / g.frames;
+  return g;
+}
+
 int64_t g2k_grad_workspace_bytes(const g2k_dims* d) {
   if (validate_common(d, true) != G2K_OK) return -1;
-  const int GW = grad_waves(d->Nmax);
-  const int64_t ngroup = (d->F + GW - 1) / GW;
+  const int64_t ngroup = grad_launch(d).ngroup;
   return ((int64_t)d->S * ngroup + kGradSlices) * (grad_params(d->Nmax) + 2) * 4;
 }
 
@@ -3218,8 +3607,8 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
   if (!workspace || workspace_bytes < need)
     return set_err(G2K_EINVAL, "workspace of %lld bytes needed (got %lld)", (long long)need,
                    (long long)workspace_bytes);
-  const int GW = grad_waves(d->Nmax);
-  const int ngroup = (d->F + GW - 1) / GW;
+  const GradLaunch gl = grad_launch(d);
+  const int GW = gl.frames, ngroup = gl.ngroup;
   const int width = grad_params(d->Nmax) + 2;
   hipStream_t st = (hipStream_t)stream;
   if (d->S == 0 || ngroup == 0) {
@@ -3227,7 +3616,8 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
       return set_err(G2K_ELAUNCH, "g2k_step_grad_f32: memset failed");
     return G2K_OK;
   }
-  const size_t lds = (size_t)4 * (grad_shared_floats(d->Nmax) + GW * grad_scratch_floats(d->Nmax));
+  const size_t lds = gl.seq ? (size_t)4 * grad_seq_lds_floats(d->Nmax)
+                            : (size_t)4 * (grad_shared_floats(d->Nmax) + GW * grad_scratch_floats(d->Nmax));
   if (lds > 160 * 1024) return set_err(G2K_ELDS, "Nmax=%d needs %zu bytes of LDS", d->Nmax, lds);
   GradArgs a;
   a.d = *d; a.w = *w; a.pos = pos; a.vislet = vislet; a.G = G; a.targets = targets;
@@ -3235,7 +3625,9 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
   a.part = static_cast<float*>(workspace); a.ngroup = ngroup;
   float* red = a.part + (size_t)d->S * ngroup * width;
   const dim3 grid(ngroup, d->S);
-  if (GW == 4)
+  if (gl.seq)
+    hipLaunchKernelGGL(g2k_grad_seq_kernel, grid, dim3(256), lds, st, a, GW);
+  else if (GW == 4)
     hipLaunchKernelGGL((g2k_grad_kernel<4>), grid, dim3(256), lds, st, a);
   else if (GW == 2)
     hipLaunchKernelGGL((g2k_grad_kernel<2>), grid, dim3(128), lds, st, a);
