@@ -2800,6 +2800,17 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
   for (int n = tid; n < Nmax; n += NT) sAct[n] = (n < nact && (pm ? pm[n] != 0 : true)) ? 1.f : 0.f;
   for (int p = tid; p < P2; p += NT) racc[p] = 0.f;
   const GradOff go = grad_off(Nmax);
+  // the weights enter each frame only through K1 = Wv[:, :16] @ Wii (E = K1 U
+  // + Wv[:, 16:] Ve + bv, dU = K1^T dE), so the weight-side gradients need
+  // only sums over the group's frames, expanded once after the loop:
+  //   dWv[:, :16] = (sum dE U^T) Wii^T   dWii = Wv[:, :16]^T (sum dE U^T)
+  //   dWv[:, 16:] = (sum dE) Ve^T        dbv = column sums of (sum dE)
+  //   dWi += vislet^T (Wv[:, 16:]^T sum dE)
+  // They live in the X0 block of the scratch (X0 itself is never formed).
+  float* sK1 = w.X;                                   // [T][T]
+  float* sAU = w.X + kT * kT;                         // [T][T]  sum dE U^T
+  float* sSE = w.X + 2 * kT * kT;                     // [T][D]  sum dE
+  for (int o = tid; o < kT * kT + kT * kD; o += NT) sAU[o] = 0.f;
 
   for (int k = 0; k < nfg; ++k) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2813,7 +2824,15 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
       const float2 q = *reinterpret_cast<const float2*>(w.pos + t * 2 * Nmax + 2 * n);
       w.B[t * NP1 + n] = n < nact ? sqrtf(fmaf(q.x, q.x, q.y * q.y)) : 0.f;
     }
+    if (k == 0 && tid < kT * kT) {                    // K1 = Wv[:, :16] @ Wii
+      const int t = tid >> 3, u = tid & 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < kD; ++c) acc = fmaf(sWv[t * (kD + 2) + c], sWii[c * kT + u], acc);
+      sK1[tid] = acc;
+    }
     __syncthreads();
+    STAMP(20);
     if (wv == 0) {                                    // U = Bv @ Wi; Ve = vislet @ Wi (MFMA,
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};              // rows r < 10 of one 16 x 16 tile, K = n)
       const float* arow = L16 < kT ? w.B + L16 * NP1 : sVis + (L16 < kT + 2 ? L16 - kT : 0) * NP1;
@@ -2832,22 +2851,18 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
       }
     }
     __syncthreads();
-    {                                                 // X0 = Wii @ U (256 outputs)
-      const int r = tid >> 4, d = tid & 15;
-      float acc = 0.f;
-#pragma unroll
-      for (int t = 0; t < kT; ++t) acc = fmaf(sWii[r * kT + t], w.U[t * kD + d], acc);
-      w.X[tid] = acc;
-    }
-    __syncthreads();
-    if (tid < kT * kD) {                              // E = Wv @ X + bv
+    STAMP(21);
+    if (tid < kT * kD) {                              // E = K1 @ U + Wv[:, 16:] @ Ve + bv
       const int t = tid >> 4, d = tid & 15;
       float acc = sbv[d];
 #pragma unroll
-      for (int c = 0; c < kD + 2; ++c) acc = fmaf(sWv[t * (kD + 2) + c], w.X[c * kD + d], acc);
+      for (int u = 0; u < kT; ++u) acc = fmaf(sK1[t * kT + u], w.U[u * kD + d], acc);
+      acc = fmaf(sWv[t * (kD + 2) + kD], w.X[kD * kD + d], acc);
+      acc = fmaf(sWv[t * (kD + 2) + kD + 1], w.X[(kD + 1) * kD + d], acc);
       w.E[tid] = acc;
     }
     __syncthreads();
+    STAMP(22);
     if (tid < kT * kT) {                              // cost = E @ (lambda G)
       const int t = tid >> 3, u = tid & 7;
       float acc = 0.f;
@@ -2856,6 +2871,7 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
       w.C[tid] = a.lambda * acc;
     }
     __syncthreads();
+    STAMP(24);
     if (tid < kL2 * kT) {                             // M = Wc @ cost
       const int r = tid >> 3, t = tid & 7;
       float acc = 0.f;
@@ -2864,6 +2880,7 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
       w.M[tid] = acc;
     }
     __syncthreads();
+    STAMP(25);
     // dY = Y - target on active, masked pedestrians (Y = M @ Wo, :122-124)
     float lsum = 0.f, cnt = 0.f;
     for (int it = wv; it < 2 * ntile; it += 4) {      // Y tiles (MFMA): rows r, 16 pedestrians
@@ -2902,6 +2919,7 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
       sLoss[2 * wv + 1] = cnt;
     }
     __syncthreads();
+    STAMP(26);
     if (wv < 2) {                                     // dM = dY @ Wo^T (MFMA, K = n)
       const int ra = wv * 16 + L16;
       const int oa = ra < kL2 ? ((ra < kL) ? 2 * ra : 2 * (ra - kL) + 1) : 0;
@@ -2938,6 +2956,7 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
       }
     }
     __syncthreads();
+    STAMP(27);
     if (tid < kT * kT) {                              // dcost = Wc^T @ dM
       const int u = tid >> 3, t = tid & 7;
       float acc = 0.f;
@@ -2951,6 +2970,7 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
       w.gWc[p] = acc;
     }
     __syncthreads();
+    STAMP(28);
     if (tid < kT * kD) {                              // dE = dcost @ (lambda G)^T
       const int t = tid >> 4, d = tid & 15;
       float acc = 0.f;
@@ -2959,57 +2979,34 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
       w.dE[tid] = a.lambda * acc;
     }
     __syncthreads();
-    for (int o = tid; o < (kD + 2) * kD + kT * (kD + 2) + kD; o += NT) {
-      if (o < (kD + 2) * kD) {                        // dX = Wv^T @ dE
-        const int c = o >> 4, d = o & 15;
+    STAMP(29);
+    if (tid < kT * kD) {                              // dU = K1^T @ dE
+      const int u = tid >> 4, d = tid & 15;
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < kT; ++t) acc = fmaf(sK1[t * kT + u], w.dE[t * kD + d], acc);
+      w.dU[tid] = acc;
+    } else {
+      const int o = tid - kT * kD;                    // 0..127
+      sSE[o] += w.dE[o];                              // sum dE
+      if (o < kT * kT) {                              // sum dE U^T
+        const int t = o >> 3, u = o & 7;
         float acc = 0.f;
 #pragma unroll
-        for (int t = 0; t < kT; ++t) acc = fmaf(sWv[t * (kD + 2) + c], w.dE[t * kD + d], acc);
-        w.dX[o] = acc;
-      } else if (o < (kD + 2) * kD + kT * (kD + 2)) { // dWv = dE @ X^T
-        const int p = o - (kD + 2) * kD, t = p / (kD + 2), c = p - t * (kD + 2);
-        float acc = 0.f;
-#pragma unroll
-        for (int d = 0; d < kD; ++d) acc = fmaf(w.dE[t * kD + d], w.X[c * kD + d], acc);
-        w.gWv[p] = acc;
-      } else {                                        // dbv = column sums of dE
-        const int d = o - (kD + 2) * kD - kT * (kD + 2);
-        float acc = 0.f;
-#pragma unroll
-        for (int t = 0; t < kT; ++t) acc += w.dE[t * kD + d];
-        w.gbv[d] = acc;
+        for (int d = 0; d < kD; ++d) acc = fmaf(w.dE[t * kD + d], w.U[u * kD + d], acc);
+        sAU[o] += acc;
       }
     }
     __syncthreads();
-    if (tid < kT * kD) {                              // dU = Wii^T @ dX0
-      const int t = tid >> 4, d = tid & 15;
-      float acc = 0.f;
-#pragma unroll
-      for (int r = 0; r < kD; ++r) acc = fmaf(sWii[r * kT + t], w.dX[r * kD + d], acc);
-      w.dU[tid] = acc;
-    } else {                                          // dWii = dX0 @ U^T (128 outputs)
-      const int p = tid - kT * kD, r = p >> 3, t = p & 7;
-      float acc = 0.f;
-#pragma unroll
-      for (int d = 0; d < kD; ++d) acc = fmaf(w.dX[r * kD + d], w.U[t * kD + d], acc);
-      w.gWii[p] = acc;
-    }
-    __syncthreads();
-    for (int nt = wv; nt < ntile; nt += 4) {          // dWi += [Bv; vislet]^T @ [dU; dVe] (MFMA)
+    STAMP(30);
+    for (int nt = wv; nt < ntile; nt += 4) {          // dWi += Bv^T @ dU (MFMA)
       const int na = nt * 16 + L16;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 3; ++ks) {
-        const int kk = 4 * ks + q4;                  // 8 window rows, 2 vislet rows, 2 zero
-        float av = 0.f, bv = 0.f;
-        if (kk < kT) {
-          av = na < nact ? w.B[kk * NP1 + na] : 0.f;
-          bv = w.dU[kk * kD + L16];
-        } else if (kk < kT + 2) {
-          av = na < nact ? sVis[(kk - kT) * NP1 + na] : 0.f;
-          bv = w.dX[(kD + kk - kT) * kD + L16];
-        }
-        acc = mfma4(av, bv, acc);
+      for (int ks = 0; ks < 2; ++ks) {                // the 8 window rows
+        const int kk = 4 * ks + q4;
+        const float av = na < nact ? w.B[kk * NP1 + na] : 0.f;
+        acc = mfma4(av, w.dU[kk * kD + L16], acc);
       }
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -3017,28 +3014,55 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
         if (n < Nmax) racc[go.wi + n * kD + L16] += acc[v];
       }
     }
-    for (int p = go.wii + tid; p < P2; p += NT) {     // the rest of this frame's row
-      if (p >= go.wo && p < P) continue;              // dWo: accumulated by the MFMA tiles
-      float c;
-      if (p < go.wv) {
-        c = w.gWii[p - go.wii];
-      } else if (p < go.bv) {
-        c = w.gWv[p - go.wv];
-      } else if (p < go.wr) {
-        c = w.gbv[p - go.bv];
-      } else if (p < go.wc) {
-        c = 0.f;                                      // Wr does not reach pred
-      } else if (p < go.wo) {
-        c = w.gWc[p - go.wc];
+    for (int p = tid; p < kL2 * kT + 2; p += NT) {    // dWc, loss and count of this frame
+      if (p < kL2 * kT) {
+        racc[go.wc + p] += w.gWc[p];
       } else {
-        const int j = p - P;                          // loss, count: waves in order
-        c = ((sLoss[j] + sLoss[2 + j]) + sLoss[4 + j]) + sLoss[6 + j];
+        const int j = p - kL2 * kT;                   // waves in order
+        racc[P + j] += ((sLoss[j] + sLoss[2 + j]) + sLoss[4 + j]) + sLoss[6 + j];
       }
-      racc[p] += c;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA outlives the workgroup
   __syncthreads();
+  if (nfg > 0) {                                      // the weight-side gradients of the group
+    float* sdVe = w.dX;                               // [2][D] Wv[:, 16:]^T sum dE
+    for (int o = tid; o < kT * (kD + 2) + kD * kT + kD + 2 * kD; o += NT) {
+      float acc = 0.f;
+      if (o < kT * (kD + 2)) {                        // dWv
+        const int t = o / (kD + 2), c = o - t * (kD + 2);
+        if (c < kD) {
+#pragma unroll
+          for (int u = 0; u < kT; ++u) acc = fmaf(sAU[t * kT + u], sWii[c * kT + u], acc);
+        } else {
+#pragma unroll
+          for (int d = 0; d < kD; ++d) acc = fmaf(sSE[t * kD + d], w.X[c * kD + d], acc);
+        }
+        racc[go.wv + o] = acc;
+      } else if (o < kT * (kD + 2) + kD * kT) {       // dWii
+        const int q = o - kT * (kD + 2), c = q >> 3, u = q & 7;
+#pragma unroll
+        for (int t = 0; t < kT; ++t) acc = fmaf(sWv[t * (kD + 2) + c], sAU[t * kT + u], acc);
+        racc[go.wii + q] = acc;
+      } else if (o < kT * (kD + 2) + kD * kT + kD) {  // dbv
+        const int d = o - kT * (kD + 2) - kD * kT;
+#pragma unroll
+        for (int t = 0; t < kT; ++t) acc += sSE[t * kD + d];
+        racc[go.bv + d] = acc;
+      } else {                                        // dVe
+        const int q = o - kT * (kD + 2) - kD * kT - kD, j = q >> 4, d = q & 15;
+#pragma unroll
+        for (int t = 0; t < kT; ++t) acc = fmaf(sWv[t * (kD + 2) + kD + j], sSE[t * kD + d], acc);
+        sdVe[q] = acc;
+      }
+    }
+    __syncthreads();
+    for (int p = tid; p < nact * kD; p += NT) {       // dWi += vislet^T @ dVe
+      const int n = p >> 4, d = p & 15;
+      racc[go.wi + p] += fmaf(sVis[n], sdVe[d], sVis[NP1 + n] * sdVe[kD + d]);
+    }
+    __syncthreads();
+  }
   float* row = a.part + ((size_t)s * a.ngroup + grp) * (size_t)P2;
   for (int p = tid; p < P2; p += NT) row[p] = racc[p];
   STAMP(32);
@@ -3051,8 +3075,8 @@ __global__ void __launch_bounds__(256) g2k_grad_reduce1_kernel(const float* __re
   const int p = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y;
   if (p >= width) return;
   float acc = 0.f;
-#pragma unroll 4
-  for (int r = k; r < rows; r += kGradSlices) acc += part[(size_t)r * width + p];
+#pragma unroll 16
+  for (int r = k; r < rows; r += kGradSlices) acc += part[(size_t)r * width + p];   // loads in flight
   red[(size_t)k * width + p] = acc;
 }
 
@@ -3061,9 +3085,12 @@ __global__ void __launch_bounds__(256) g2k_grad_reduce2_kernel(const float* __re
                                                                float* __restrict__ grad, int width) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= width) return;
+  float v[kGradSlices];                             // every slice's load in flight at once
+#pragma unroll
+  for (int k = 0; k < kGradSlices; ++k) v[k] = red[(size_t)k * width + p];
   float acc = 0.f;
-#pragma unroll 8
-  for (int k = 0; k < kGradSlices; ++k) acc += red[(size_t)k * width + p];
+#pragma unroll
+  for (int k = 0; k < kGradSlices; ++k) acc += v[k];
   grad[p] = acc;
 }
 
@@ -3078,11 +3105,33 @@ __global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ pa
                                                           float lr, float decay, float clip) {
   __shared__ float red[16];
   const int tid = threadIdx.x;
+  // up to kPre entries per thread: parameters and mean squares are loaded
+  // together with the gradient, before the norm's reduction
+  constexpr int kPre = 8;
+  const bool pre = n <= kPre * 1024;
+  float pg[kPre], pp[kPre], pm[kPre];
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int i = tid + j * 1024;
+      pg[j] = i < n ? grad[i] : 0.f;
+      pp[j] = i < n ? params[i] : 0.f;
+      pm[j] = (ms && i < n) ? ms[i] : 0.f;
+    }
+  }
   const float inv = 1.0f / fmaxf(grad[n + 1], 1.0f);
   float ss = 0.f;
-  for (int i = tid; i < n; i += 1024) {
-    const float g = grad[i] * inv;
-    ss = fmaf(g, g, ss);
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const float g = pg[j] * inv;
+      ss = fmaf(g, g, ss);
+    }
+  } else {
+    for (int i = tid; i < n; i += 1024) {
+      const float g = grad[i] * inv;
+      ss = fmaf(g, g, ss);
+    }
   }
   ss = wave_sum(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
@@ -3092,6 +3141,22 @@ __global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ pa
   for (int w = 0; w < 16; ++w) tot += red[w];
   const float nrm = sqrtf(tot);
   const float scale = clip > 0.f ? inv * (clip / fmaxf(nrm, clip)) : inv;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int i = tid + j * 1024;
+      if (i >= n) break;
+      const float g = pg[j] * scale;
+      if (ms) {
+        const float m = fmaf(decay, pm[j], (1.f - decay) * g * g);
+        ms[i] = m;
+        params[i] = pp[j] - lr * g / sqrtf(m + 1e-10f);
+      } else {
+        params[i] = fmaf(-lr, g, pp[j]);
+      }
+    }
+    return;
+  }
   for (int i = tid; i < n; i += 1024) {
     const float g = grad[i] * scale;
     if (ms) {

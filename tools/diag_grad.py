@@ -23,9 +23,7 @@ def plan():
 
 
 ref = None
-variants = [("seq", {}), ("seq fpg2", {"G2K_GRAD_FPG": "2"}), ("seq fpg4", {"G2K_GRAD_FPG": "4"}),
-            ("seq fpg10", {"G2K_GRAD_FPG": "10"}), ("wave GW4", {"G2K_GRAD_GW": "4"}),
-            ("wave GW2", {"G2K_GRAD_GW": "2"})]
+variants = [("seq", {}), ("wave GW4", {"G2K_GRAD_GW": "4"})]
 for name, env in variants:
     for k in ("G2K_GRAD_GW", "G2K_GRAD_FPG"):
         os.environ.pop(k, None)
@@ -61,5 +59,9 @@ st = (ctypes.c_ulonglong * 64)()
 lib.g2k_debug_stamps(st, 64)
 v = np.array(st[18:33], dtype=np.int64)
 print("seq kernel WG(0,0): start->last frame top", int(v[1] - v[0]), "start->end", int(v[14] - v[0]))
-names = ["start", "dma+sync", "B", "U/Ve", "X0", "E", "C", "M", "dY", "dM", "dC/dWc", "dE",
-         "dX/dWv", "dU+sync", "row"]
+idx = [19, 20, 21, 22, 24, 25, 26, 27, 28, 29, 30]
+names = ["top", "B", "U/Ve", "E", "C", "M", "dY", "dM/dWo", "dC/dWc", "dE", "dU/sums"]
+w = np.array([st[i] for i in idx], dtype=np.int64)
+print("seq kernel WG(0,0), last frame, phase cycles:",
+      ", ".join(f"{names[i]} {w[i] - w[i - 1]}" for i in range(1, len(w))),
+      "| row + expansion", int(st[32] - st[30]))
