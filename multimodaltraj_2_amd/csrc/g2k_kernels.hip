@@ -2711,14 +2711,16 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
 // order: the same sums as g2k_grad_kernel's wave-order sum).  One scratch
 // instead of one per wave: ~31 KB of LDS at Nmax = 32, five workgroups per
 // CU, so every (scene, group) of eth_hotel_synth is resident at once.
+// workgroups per CU the register budget allows (one wave per SIMD each)
+constexpr int kGradSeqWgPerCu = 5;
 __host__ __device__ inline int grad_seq_buf_floats(int Nmax) { return (2 * kT + kL2) * Nmax; }
 __host__ __device__ inline int grad_seq_lds_floats(int Nmax) {
   return grad_shared_floats(Nmax) + grad_scratch_floats(Nmax) + 8 + grad_seq_buf_floats(Nmax)
-         + grad_params(Nmax) + 2 + Nmax;
+         + grad_params(Nmax) + 2 + Nmax + 4 * 256;
 }
 // frames per workgroup: the workgroups run in ceil(groups / slots) rounds of
 // `fpg` sequential frames each (slots = CUs x resident workgroups per CU, by
-// LDS and by the 5-wave-per-SIMD register bound); minimise rounds x fpg,
+// LDS and by the register bound kGradSeqWgPerCu); minimise rounds x fpg,
 // ties to the larger fpg (fewer prologues and partial rows)
 static int grad_cu_count() {
   static int cus = 0;
@@ -2737,7 +2739,7 @@ inline int grad_seq_fpg(const g2k_dims* d) {
     if (v >= 1 && v <= 64) return v;
   }
   int per_cu = (160 * 1024) / (4 * grad_seq_lds_floats(d->Nmax));
-  per_cu = per_cu < 1 ? 1 : (per_cu > 5 ? 5 : per_cu);
+  per_cu = per_cu < 1 ? 1 : (per_cu > kGradSeqWgPerCu ? kGradSeqWgPerCu : per_cu);
   const int64_t slots = (int64_t)grad_cu_count() * per_cu;
   int best = 1;
   int64_t best_cost = -1;
@@ -2749,7 +2751,7 @@ inline int grad_seq_fpg(const g2k_dims* d) {
   return best;
 }
 
-__global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fpg) {
+__global__ void __launch_bounds__(256, kGradSeqWgPerCu) g2k_grad_seq_kernel(GradArgs a, int fpg) {
   constexpr int NT = 256;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int Nmax = a.d.Nmax, F = a.d.F, P = grad_params(Nmax), P2 = P + 2;
@@ -2770,6 +2772,7 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
   float* buf[2] = {w.pos, sLoss + 8};                 // pos window then targets, per frame
   float* racc = buf[1] + grad_seq_buf_floats(Nmax);  // [P + 2] this group's row
   float* sAct = racc + P2;                            // [Nmax] 1 for active, masked pedestrians
+  float* sUp = sAct + Nmax;                           // [4 waves][16][16] partial U/Ve tiles
   const int f0 = grp * fpg;
   const int L16 = lane & 15, q4 = lane >> 4;          // MFMA 16x16x4 lane roles
   const int ntile = (Nmax + 15) >> 4;                 // 16-pedestrian tiles
@@ -2833,10 +2836,11 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
     }
     __syncthreads();
     STAMP(20);
-    if (wv == 0) {                                    // U = Bv @ Wi; Ve = vislet @ Wi (MFMA,
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};              // rows r < 10 of one 16 x 16 tile, K = n)
-      const float* arow = L16 < kT ? w.B + L16 * NP1 : sVis + (L16 < kT + 2 ? L16 - kT : 0) * NP1;
-      for (int n0 = 0; n0 < nact; n0 += 4) {
+    {                                                 // U = Bv @ Wi; Ve = vislet @ Wi (MFMA:
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};              // rows r < 10 of one 16 x 16 tile, the
+      const float* arow = L16 < kT ? w.B + L16 * NP1 // K = n steps split over the waves)
+                                   : sVis + (L16 < kT + 2 ? L16 - kT : 0) * NP1;
+      for (int n0 = 4 * wv; n0 < nact; n0 += 16) {
         const int n = n0 + q4;
         const bool ok = n < nact;
         const float av = (ok && L16 < kT + 2) ? arow[n] : 0.f;
@@ -2844,22 +2848,24 @@ __global__ void __launch_bounds__(256, 5) g2k_grad_seq_kernel(GradArgs a, int fp
         acc = mfma4(av, bv, acc);
       }
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int r = 4 * q4 + v;
-        if (r < kT) w.U[r * kD + L16] = acc[v];
-        else if (r < kT + 2) w.X[(kD + r - kT) * kD + L16] = acc[v];
-      }
+      for (int v = 0; v < 4; ++v) sUp[wv * 256 + (4 * q4 + v) * 16 + L16] = acc[v];
     }
     __syncthreads();
     STAMP(21);
+    // the waves' partial tiles summed in wave order (one rounding for everyone)
+    auto usum = [&](int o) { return ((sUp[o] + sUp[256 + o]) + sUp[512 + o]) + sUp[768 + o]; };
     if (tid < kT * kD) {                              // E = K1 @ U + Wv[:, 16:] @ Ve + bv
       const int t = tid >> 4, d = tid & 15;
       float acc = sbv[d];
 #pragma unroll
-      for (int u = 0; u < kT; ++u) acc = fmaf(sK1[t * kT + u], w.U[u * kD + d], acc);
-      acc = fmaf(sWv[t * (kD + 2) + kD], w.X[kD * kD + d], acc);
-      acc = fmaf(sWv[t * (kD + 2) + kD + 1], w.X[(kD + 1) * kD + d], acc);
+      for (int u = 0; u < kT; ++u) acc = fmaf(sK1[t * kT + u], usum(u * kD + d), acc);
+      acc = fmaf(sWv[t * (kD + 2) + kD], usum(kD * kT + d), acc);
+      acc = fmaf(sWv[t * (kD + 2) + kD + 1], usum(kD * (kT + 1) + d), acc);
       w.E[tid] = acc;
+    } else {                                          // U, and Ve into X rows 16, 17
+      const int o = tid - kT * kD;
+      w.U[o] = usum(o);
+      if (o < 2 * kD) w.X[kD * kD + o] = usum(kD * kT + o);
     }
     __syncthreads();
     STAMP(22);
