@@ -2822,10 +2822,20 @@ __global__ void __launch_bounds__(256, kGradSeqWgPerCu) g2k_grad_seq_kernel(Grad
     w.pos = buf[k & 1];
     w.tgt = w.pos + kT * 2 * Nmax;
     if (k + 1 < nfg) dma_frame(f0 + k + 1, buf[(k + 1) & 1]);
-    for (int i = tid; i < kT * Nmax; i += NT) {       // a2 window norms (train.py:76-85)
-      const int t = i / Nmax, n = i - t * Nmax;
-      const float2 q = *reinterpret_cast<const float2*>(w.pos + t * 2 * Nmax + 2 * n);
-      w.B[t * NP1 + n] = n < nact ? sqrtf(fmaf(q.x, q.x, q.y * q.y)) : 0.f;
+    if (Nmax >= NT / 2) {                             // a2 window norms (train.py:76-85):
+      for (int n = tid; n < Nmax; n += NT) {          // one pedestrian per thread when wide,
+#pragma unroll 4
+        for (int t = 0; t < kT; ++t) {
+          const float2 q = *reinterpret_cast<const float2*>(w.pos + t * 2 * Nmax + 2 * n);
+          w.B[t * NP1 + n] = n < nact ? sqrtf(fmaf(q.x, q.x, q.y * q.y)) : 0.f;
+        }
+      }
+    } else {
+      for (int i = tid; i < kT * Nmax; i += NT) {     // else (frame row, pedestrian) pairs
+        const int t = i / Nmax, n = i - t * Nmax;
+        const float2 q = *reinterpret_cast<const float2*>(w.pos + t * 2 * Nmax + 2 * n);
+        w.B[t * NP1 + n] = n < nact ? sqrtf(fmaf(q.x, q.x, q.y * q.y)) : 0.f;
+      }
     }
     if (k == 0 && tid < kT * kT) {                    // K1 = Wv[:, :16] @ Wii
       const int t = tid >> 3, u = tid & 7;
@@ -2840,12 +2850,17 @@ __global__ void __launch_bounds__(256, kGradSeqWgPerCu) g2k_grad_seq_kernel(Grad
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};              // rows r < 10 of one 16 x 16 tile, the
       const float* arow = L16 < kT ? w.B + L16 * NP1 // K = n steps split over the waves)
                                    : sVis + (L16 < kT + 2 ? L16 - kT : 0) * NP1;
-      for (int n0 = 4 * wv; n0 < nact; n0 += 16) {
-        const int n = n0 + q4;
-        const bool ok = n < nact;
-        const float av = (ok && L16 < kT + 2) ? arow[n] : 0.f;
-        const float bv = ok ? sWi[n * kD + L16] : 0.f;
-        acc = mfma4(av, bv, acc);
+      for (int n0 = 4 * wv; n0 < nact; n0 += 64) {    // four k-steps' loads in flight
+        float av[4], bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + 16 * j + q4;
+          const bool ok = n < nact;
+          av[j] = (ok && L16 < kT + 2) ? arow[n] : 0.f;
+          bv[j] = ok ? sWi[n * kD + L16] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = mfma4(av[j], bv[j], acc);
       }
 #pragma unroll
       for (int v = 0; v < 4; ++v) sUp[wv * 256 + (4 * q4 + v) * 16 + L16] = acc[v];
@@ -2930,12 +2945,17 @@ __global__ void __launch_bounds__(256, kGradSeqWgPerCu) g2k_grad_seq_kernel(Grad
       const int ra = wv * 16 + L16;
       const int oa = ra < kL2 ? ((ra < kL) ? 2 * ra : 2 * (ra - kL) + 1) : 0;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int n0 = 0; n0 < nact; n0 += 4) {
-        const int n = n0 + q4;
-        const bool ok = n < nact;
-        const float av = (ok && ra < kL2) ? w.tgt[n * kL2 + oa] : 0.f;
-        const float bv = (ok && L16 < kT) ? sWo[L16 * NP1 + n] : 0.f;
-        acc = mfma4(av, bv, acc);
+      for (int n0 = 0; n0 < nact; n0 += 16) {         // four k-steps' loads in flight
+        float av[4], bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + 4 * j + q4;
+          const bool ok = n < nact;
+          av[j] = (ok && ra < kL2) ? w.tgt[n * kL2 + oa] : 0.f;
+          bv[j] = (ok && L16 < kT) ? sWo[L16 * NP1 + n] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = mfma4(av[j], bv[j], acc);
       }
       if (L16 < kT) {
 #pragma unroll

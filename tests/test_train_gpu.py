@@ -31,8 +31,18 @@ def _ref_grad(b, w, nfr, mask, lam):
     return loss, cnt, R
 
 
-@pytest.mark.parametrize("Nmax,F,lam", [(32, 6, 5e-4), (7, 5, 0.05), (200, 3, 0.05)])
-def test_grad_matches_oracle(gpu, Nmax, F, lam):
+# G2K_GRAD_FPG forces frames per workgroup (the launcher picks 1 for these
+# small S): groups of 2/3/8 frames exercise the prefetch double buffer, the
+# frame-order row accumulation and n_frames ending inside a group;
+# G2K_GRAD_GW selects the one-wave-per-frame kernel
+@pytest.mark.parametrize("Nmax,F,lam,env", [
+    (32, 6, 5e-4, {}), (7, 5, 0.05, {}), (200, 3, 0.05, {}),
+    (32, 7, 0.05, {"G2K_GRAD_FPG": "3"}), (20, 9, 0.05, {"G2K_GRAD_FPG": "2"}),
+    (64, 7, 5e-4, {"G2K_GRAD_FPG": "8"}), (256, 4, 0.05, {"G2K_GRAD_FPG": "3"}),
+    (32, 6, 5e-4, {"G2K_GRAD_GW": "4"}), (200, 3, 0.05, {"G2K_GRAD_GW": "2"})])
+def test_grad_matches_oracle(gpu, monkeypatch, Nmax, F, lam, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     S = 3
     b = make_batch(S, Nmax, 64, F=F, seed=21)
     mask = np.ones((S, Nmax), bool)
