@@ -220,6 +220,19 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
                       int64_t workspace_bytes, void* stream);
 int g2k_update_f32(float* params, float* ms, const float* grad, int64_t n_params, float lr,
                    float decay, float grad_clip, void* stream);
+/*
+ * g2k_step_grad_update_f32: one rank's whole train-mode update (nothing to
+ *   all-reduce): g2k_step_grad_f32 then g2k_update_f32 on params [P] (the flat
+ *   buffer in g2k_weights order, P = g2k_grad_size) with the last reduction
+ *   pass and the update in one launch.  Same results, bit for bit, as the two
+ *   calls; grad [P + 2] is still written.  Same workspace.
+ */
+int g2k_step_grad_update_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
+                             const float* vislet, const float* G, const float* targets,
+                             const int32_t* n_active, const int32_t* n_frames,
+                             const uint8_t* ped_mask, float lambda, float* grad, void* workspace,
+                             int64_t workspace_bytes, float* params, float* ms, float lr,
+                             float decay, float grad_clip, void* stream);
 
 /*
  * g2k_context_conv_f32 — the static-context input (a5).

@@ -53,6 +53,9 @@ SYMBOLS = {
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp,
                                   c_i64, c_vp]),
     "g2k_update_f32": (c_int, [c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_vp]),
+    "g2k_step_grad_update_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
+                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp,
+                                         c_vp, c_i64, c_vp, c_vp, c_f32, c_f32, c_f32, c_vp]),
     "g2k_context_conv_workspace_bytes": (c_i64, [c_i32, c_i32, c_i32]),
     "g2k_context_conv_f32": (c_int, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp,
                                      c_vp, c_i64, c_vp]),

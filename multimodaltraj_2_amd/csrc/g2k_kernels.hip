@@ -3125,10 +3125,9 @@ __global__ void __launch_bounds__(256) g2k_grad_reduce2_kernel(const float* __re
 // then RMSProp (ms = decay ms + (1 - decay) g^2; p -= lr g / sqrt(ms +
 // 1e-10), TF RMSPropOptimizer without momentum) or SGD (ms NULL).  One
 // workgroup: the norm is a fixed-order block reduction.
-__global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ params,
-                                                          float* __restrict__ ms,
-                                                          const float* __restrict__ grad, int n,
-                                                          float lr, float decay, float clip) {
+__device__ __forceinline__ void update_apply(float* __restrict__ params, float* __restrict__ ms,
+                                             const float* __restrict__ grad, int n, float lr,
+                                             float decay, float clip) {
   __shared__ float red[16];
   const int tid = threadIdx.x;
   // up to kPre entries per thread: parameters and mean squares are loaded
@@ -3193,6 +3192,34 @@ __global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ pa
       params[i] = fmaf(-lr, g, params[i]);
     }
   }
+}
+
+__global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ params,
+                                                          float* __restrict__ ms,
+                                                          const float* __restrict__ grad, int n,
+                                                          float lr, float decay, float clip) {
+  update_apply(params, ms, grad, n, lr, decay, clip);
+}
+
+// one rank (nothing to all-reduce): the second reduction pass and the update
+// in one workgroup — the same slice sums as g2k_grad_reduce2_kernel (grad is
+// still written), then the same update as g2k_update_kernel
+__global__ void __launch_bounds__(1024) g2k_reduce2_update_kernel(const float* __restrict__ slices,
+                                                                  float* __restrict__ grad, int width,
+                                                                  float* __restrict__ params,
+                                                                  float* __restrict__ ms, int n,
+                                                                  float lr, float decay, float clip) {
+  for (int p = threadIdx.x; p < width; p += 1024) {
+    float v[kGradSlices];
+#pragma unroll
+    for (int k = 0; k < kGradSlices; ++k) v[k] = slices[(size_t)k * width + p];
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < kGradSlices; ++k) acc += v[k];
+    grad[p] = acc;
+  }
+  __syncthreads();   // the workgroup's grad stores are visible to the whole workgroup
+  update_apply(params, ms, grad, n, lr, decay, clip);
 }
 
 // ---------------------------------------------------------------------------
@@ -3680,11 +3707,12 @@ int64_t g2k_grad_workspace_bytes(const g2k_dims* d) {
   return ((int64_t)d->S * ngroup + kGradSlices) * (grad_params(d->Nmax) + 2) * 4;
 }
 
-int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
-                      const float* vislet, const float* G, const float* targets,
-                      const int32_t* n_active, const int32_t* n_frames, const uint8_t* ped_mask,
-                      float lambda, float* grad, void* workspace, int64_t workspace_bytes,
-                      void* stream) {
+static int step_grad(const g2k_dims* d, const g2k_weights* w, const float* pos,
+                     const float* vislet, const float* G, const float* targets,
+                     const int32_t* n_active, const int32_t* n_frames, const uint8_t* ped_mask,
+                     float lambda, float* grad, void* workspace, int64_t workspace_bytes,
+                     void* stream, float* upd_params, float* upd_ms, float lr, float decay,
+                     float grad_clip) {
   int rc = validate_common(d, true);
   if (rc) return rc;
   if ((rc = validate_weights(w, true))) return rc;
@@ -3705,7 +3733,10 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
   if (d->S == 0 || ngroup == 0) {
     if (hipMemsetAsync(grad, 0, (size_t)width * 4, st) != hipSuccess)
       return set_err(G2K_ELAUNCH, "g2k_step_grad_f32: memset failed");
-    return G2K_OK;
+    if (upd_params)
+      hipLaunchKernelGGL(g2k_update_kernel, dim3(1), dim3(1024), 0, st, upd_params, upd_ms, grad,
+                         width - 2, lr, decay, grad_clip);
+    return check_launch("g2k_step_grad_f32/empty");
   }
   const size_t lds = gl.seq ? (size_t)4 * grad_seq_lds_floats(d->Nmax)
                             : (size_t)4 * (grad_shared_floats(d->Nmax) + GW * grad_scratch_floats(d->Nmax));
@@ -3728,8 +3759,32 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
   const unsigned gx = (unsigned)((width + 255) / 256);
   hipLaunchKernelGGL(g2k_grad_reduce1_kernel, dim3(gx, kGradSlices), dim3(256), 0, st, a.part, red,
                      d->S * ngroup, width);
-  hipLaunchKernelGGL(g2k_grad_reduce2_kernel, dim3(gx), dim3(256), 0, st, red, grad, width);
+  if (upd_params)
+    hipLaunchKernelGGL(g2k_reduce2_update_kernel, dim3(1), dim3(1024), 0, st, red, grad, width,
+                       upd_params, upd_ms, width - 2, lr, decay, grad_clip);
+  else
+    hipLaunchKernelGGL(g2k_grad_reduce2_kernel, dim3(gx), dim3(256), 0, st, red, grad, width);
   return check_launch("g2k_step_grad_f32/reduce");
+}
+
+int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
+                      const float* vislet, const float* G, const float* targets,
+                      const int32_t* n_active, const int32_t* n_frames, const uint8_t* ped_mask,
+                      float lambda, float* grad, void* workspace, int64_t workspace_bytes,
+                      void* stream) {
+  return step_grad(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda, grad,
+                   workspace, workspace_bytes, stream, nullptr, nullptr, 0.f, 0.f, 0.f);
+}
+
+int g2k_step_grad_update_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
+                             const float* vislet, const float* G, const float* targets,
+                             const int32_t* n_active, const int32_t* n_frames,
+                             const uint8_t* ped_mask, float lambda, float* grad, void* workspace,
+                             int64_t workspace_bytes, float* params, float* ms, float lr,
+                             float decay, float grad_clip, void* stream) {
+  if (!params) return set_err(G2K_EINVAL, "params is NULL");
+  return step_grad(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda, grad,
+                   workspace, workspace_bytes, stream, params, ms, lr, decay, grad_clip);
 }
 
 int g2k_update_f32(float* params, float* ms, const float* grad, int64_t n_params, float lr,

@@ -88,6 +88,7 @@ class GradPlan:
         self._ws = torch.empty(max(nws, 256), dtype=torch.uint8, device=dev)
         w = params.abi()
         self._fn = lib.g2k_step_grad_f32
+        self._fused = lib.g2k_step_grad_update_f32
         self._args = (ctypes.byref(d), ctypes.byref(w), _ptr(pos), _ptr(vislet), _ptr(G),
                       _ptr(targets), _ptr(n_active), _ptr(n_frames), _ptr(ped_mask),
                       ctypes.c_float(lam), self.grad.data_ptr(), self._ws.data_ptr(), nws,
@@ -98,6 +99,21 @@ class GradPlan:
         rc = self._fn(*self._args)
         if rc:
             _lib.check("g2k_step_grad_f32", rc)
+        return self.grad
+
+    def run_update(self, flat, ms, *, lr, decay, grad_clip) -> torch.Tensor:
+        """One rank: the gradient and the update of ``flat`` (and ``ms``) in
+        one call (g2k_step_grad_update_f32; the same results as ``run()`` +
+        ``optimizer_update``, one launch fewer)."""
+        if flat.numel() != self.P:
+            raise ValueError(f"flat must have {self.P} entries")
+        if ms is not None and ms.numel() != self.P:
+            raise ValueError(f"ms must have {self.P} entries")
+        rc = self._fused(*self._args[:-1], flat.data_ptr(),
+                         None if ms is None else ms.data_ptr(), float(lr), float(decay),
+                         float(grad_clip), self._args[-1])
+        if rc:
+            _lib.check("g2k_step_grad_update_f32", rc)
         return self.grad
 
 
@@ -141,6 +157,9 @@ class TrainStep:
     def run(self) -> torch.Tensor:
         """Returns the (all-rank) [P + 2] buffer: gradient sums, loss, count."""
         self.fwd.run()
+        if self.world == 1:                            # nothing to all-reduce: fused update
+            return self.gradplan.run_update(self.flat, self.ms, lr=self.lr, decay=self.decay,
+                                            grad_clip=self.grad_clip)
         g = self.gradplan.run()
         if self.world > 1:
             allreduce_grad(g, self.group)

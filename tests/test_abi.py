@@ -107,6 +107,13 @@ def test_gridlstm_and_train_entry_points_validate():
                                None, 5e-4, p, p, need, None)
     assert rc == -4
     assert lib.g2k_update_f32(None, None, p, 10, 0.1, 0.9, 10.0, None) == -1
+    # the one-rank fused gradient + update: NULL params, short workspace
+    rc = lib.g2k_step_grad_update_f32(ctypes.byref(d), ctypes.byref(w), p, p, p, p, p, None, None,
+                                      5e-4, p, p, need, None, None, 5e-3, 0.95, 10.0, None)
+    assert rc == -1 and b"params" in lib.g2k_last_error()
+    rc = lib.g2k_step_grad_update_f32(ctypes.byref(d), ctypes.byref(w), p, p, p, p, p, None, None,
+                                      5e-4, p, p, need - 4, p, None, 5e-3, 0.95, 10.0, None)
+    assert rc == -1 and b"workspace" in lib.g2k_last_error()
     assert lib.g2k_update_f32(p, None, p, 0, 0.1, 0.9, 10.0, None) == 0
 
 

@@ -101,6 +101,32 @@ def test_update_matches_oracle(gpu, rms, clip):
         assert np.abs(ms.cpu().numpy() - rm).max() <= 1e-5 * np.abs(rm).max()
 
 
+@pytest.mark.parametrize("Nmax,S,F,rms", [(32, 8, 20, True), (7, 3, 5, False), (256, 4, 6, True),
+                                           (200, 2, 4, True)])
+def test_fused_grad_update_matches_two_calls(gpu, Nmax, S, F, rms):
+    """g2k_step_grad_update_f32 == g2k_step_grad_f32 + g2k_update_f32, bit for
+    bit (same reduction order, same update), grad [P + 2] included."""
+    b = make_batch(S, Nmax, 64, F=F, seed=9)
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    t = b.to_device(gpu)
+    out = []
+    for fused in (False, True):
+        flat, views = ts.flat_params(params)
+        ms = torch.full_like(flat, 0.25) if rms else None
+        gp = ts.GradPlan(views, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
+                         lam=0.05)
+        if fused:
+            g = gp.run_update(flat, ms, lr=5e-3, decay=0.95, grad_clip=10.0)
+        else:
+            g = gp.run()
+            ts.optimizer_update(flat, g, lr=5e-3, decay=0.95, grad_clip=10.0, ms=ms)
+        torch.cuda.synchronize()
+        out.append((g.clone(), flat.clone(), None if ms is None else ms.clone()))
+    (g0, p0, m0), (g1, p1, m1) = out
+    assert torch.equal(g0, g1) and torch.equal(p0, p1)
+    assert m0 is None or torch.equal(m0, m1)
+
+
 def test_train_step_reduces_loss(gpu):
     b = make_batch(16, 32, 128, seed=8)
     params = fs.init_params(32, seed=0, device=gpu)
