@@ -2751,7 +2751,12 @@ inline int grad_seq_fpg(const g2k_dims* d) {
   return best;
 }
 
-__global__ void __launch_bounds__(256, kGradSeqWgPerCu) g2k_grad_seq_kernel(GradArgs a, int fpg) {
+// WPE: resident workgroups per CU the build targets (one wave per SIMD each):
+// kGradSeqWgPerCu when LDS allows that many, else 2 (wide scenes, LDS-bound),
+// which leaves registers for independent MFMA chains in the K = n products
+template <int WPE>
+__global__ void __launch_bounds__(256, WPE) g2k_grad_seq_kernel(GradArgs a, int fpg) {
+  constexpr int kChains = WPE >= kGradSeqWgPerCu ? 1 : 4;
   constexpr int NT = 256;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int Nmax = a.d.Nmax, F = a.d.F, P = grad_params(Nmax), P2 = P + 2;
@@ -2847,9 +2852,11 @@ __global__ void __launch_bounds__(256, kGradSeqWgPerCu) g2k_grad_seq_kernel(Grad
     __syncthreads();
     STAMP(20);
     {                                                 // U = Bv @ Wi; Ve = vislet @ Wi (MFMA:
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};              // rows r < 10 of one 16 x 16 tile, the
+      f32x4 accs[kChains];                           // rows r < 10 of one 16 x 16 tile, the
       const float* arow = L16 < kT ? w.B + L16 * NP1 // K = n steps split over the waves)
                                    : sVis + (L16 < kT + 2 ? L16 - kT : 0) * NP1;
+#pragma unroll
+      for (int j = 0; j < kChains; ++j) accs[j] = {0.f, 0.f, 0.f, 0.f};
       for (int n0 = 4 * wv; n0 < nact; n0 += 64) {    // four k-steps' loads in flight
         float av[4], bv[4];
 #pragma unroll
@@ -2860,8 +2867,11 @@ __global__ void __launch_bounds__(256, kGradSeqWgPerCu) g2k_grad_seq_kernel(Grad
           bv[j] = ok ? sWi[n * kD + L16] : 0.f;
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = mfma4(av[j], bv[j], acc);
+        for (int j = 0; j < 4; ++j) accs[j % kChains] = mfma4(av[j], bv[j], accs[j % kChains]);
       }
+      f32x4 acc = accs[0];
+#pragma unroll
+      for (int j = 1; j < kChains; ++j) acc += accs[j];
 #pragma unroll
       for (int v = 0; v < 4; ++v) sUp[wv * 256 + (4 * q4 + v) * 16 + L16] = acc[v];
     }
@@ -2944,7 +2954,9 @@ __global__ void __launch_bounds__(256, kGradSeqWgPerCu) g2k_grad_seq_kernel(Grad
     if (wv < 2) {                                     // dM = dY @ Wo^T (MFMA, K = n)
       const int ra = wv * 16 + L16;
       const int oa = ra < kL2 ? ((ra < kL) ? 2 * ra : 2 * (ra - kL) + 1) : 0;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      f32x4 accs[kChains];                            // independent MFMA chains (wide builds)
+#pragma unroll
+      for (int j = 0; j < kChains; ++j) accs[j] = {0.f, 0.f, 0.f, 0.f};
       for (int n0 = 0; n0 < nact; n0 += 16) {         // four k-steps' loads in flight
         float av[4], bv[4];
 #pragma unroll
@@ -2955,8 +2967,11 @@ __global__ void __launch_bounds__(256, kGradSeqWgPerCu) g2k_grad_seq_kernel(Grad
           bv[j] = (ok && L16 < kT) ? sWo[L16 * NP1 + n] : 0.f;
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = mfma4(av[j], bv[j], acc);
+        for (int j = 0; j < 4; ++j) accs[j % kChains] = mfma4(av[j], bv[j], accs[j % kChains]);
       }
+      f32x4 acc = accs[0];
+#pragma unroll
+      for (int j = 1; j < kChains; ++j) acc += accs[j];
       if (L16 < kT) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
@@ -3747,8 +3762,10 @@ static int step_grad(const g2k_dims* d, const g2k_weights* w, const float* pos,
   a.part = static_cast<float*>(workspace); a.ngroup = ngroup;
   float* red = a.part + (size_t)d->S * ngroup * width;
   const dim3 grid(ngroup, d->S);
-  if (gl.seq)
-    hipLaunchKernelGGL(g2k_grad_seq_kernel, grid, dim3(256), lds, st, a, GW);
+  if (gl.seq && (160 * 1024) / lds >= (size_t)kGradSeqWgPerCu)
+    hipLaunchKernelGGL((g2k_grad_seq_kernel<kGradSeqWgPerCu>), grid, dim3(256), lds, st, a, GW);
+  else if (gl.seq)
+    hipLaunchKernelGGL((g2k_grad_seq_kernel<2>), grid, dim3(256), lds, st, a, GW);
   else if (GW == 4)
     hipLaunchKernelGGL((g2k_grad_kernel<4>), grid, dim3(256), lds, st, a);
   else if (GW == 2)
