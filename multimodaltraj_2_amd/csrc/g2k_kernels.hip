@@ -2709,8 +2709,9 @@ __global__ void __launch_bounds__(64 * GW) g2k_grad_kernel(GradArgs a) {
 // targets prefetched by LDS-DMA under the current frame's work, and the
 // group's row accumulated in LDS by the thread that owns each entry (frame
 // order: the same sums as g2k_grad_kernel's wave-order sum).  One scratch
-// instead of one per wave: ~31 KB of LDS at Nmax = 32, five workgroups per
-// CU, so every (scene, group) of eth_hotel_synth is resident at once.
+// instead of one per wave: ~34 KB of LDS at Nmax = 32, four workgroups per
+// CU, so every (scene, group) of eth_hotel_synth (5 frames each) is resident
+// at once.
 // workgroups per CU the register budget allows (one wave per SIMD each)
 constexpr int kGradSeqWgPerCu = 5;
 __host__ __device__ inline int grad_seq_buf_floats(int Nmax) { return (2 * kT + kL2) * Nmax; }
@@ -2752,8 +2753,9 @@ inline int grad_seq_fpg(const g2k_dims* d) {
 }
 
 // WPE: resident workgroups per CU the build targets (one wave per SIMD each):
-// kGradSeqWgPerCu when LDS allows that many, else 2 (wide scenes, LDS-bound),
-// which leaves registers for independent MFMA chains in the K = n products
+// kGradSeqWgPerCu when LDS allows that many, else 2 (LDS admits fewer
+// workgroups anyway), which leaves registers for independent MFMA chains in
+// the K = n products
 template <int WPE>
 __global__ void __launch_bounds__(256, WPE) g2k_grad_seq_kernel(GradArgs a, int fpg) {
   constexpr int kChains = WPE >= kGradSeqWgPerCu ? 1 : 4;
