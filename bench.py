@@ -4,22 +4,32 @@
 One step = one pass of the fused per-frame body (train.py:197-276: window
 norms, embeddings, g2k_lstm_mcr forward, attention + hidden recurrence,
 ADE/FDE sums) over one batch of synthetic ETH-shaped scenes, inputs resident
-in HBM.  Replicas only: the ADE/FDE numerators are summed across ranks once
-after the timed loop.
+in HBM.  This is "reference mode": the reference's train.py loop has no loss
+or backward (SURVEY.md finding 5).  The build's train mode (the same step +
+loss gradient + one gradient all-reduce + RMSProp) is timed beside it under
+"train_mode", with its own roofline.
 Workload = BASELINE.json configs[1]: "eth_hotel_synth" (S=256 scenes per
 rank, Nmax=32 peds, H=128, F=20 frames).  Weak scaling: every rank owns its
-own 256 scenes (seeded per rank) — no data-path collective.
+own 256 scenes (seeded per rank); reference mode has no data-path collective
+(the ADE/FDE numerators are summed across ranks once after the timed loop).
+
+Inputs rotate over K device-resident batches whose total exceeds the 256 MiB
+Infinity Cache (``--rotate``), so the HBM figure is not served on-die.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
 
-Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for the fields).
+With N > 1 and no WORLD_SIZE in the environment this process launches N
+ranks itself (``python -m torch.distributed.run``, one rank per GPU, RCCL)
+before it touches the GPU, and relays the ranks' output; a worker whose
+process group is not N ranks wide fails.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,82 +42,167 @@ sys.path.insert(0, ROOT)
 from multimodaltraj_2_amd import frame_step as fs          # noqa: E402
 from multimodaltraj_2_amd.synthetic import CONFIGS, FRAMES_PER_SCENE, make_batch  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MALL_BYTES = 256 * 2 ** 20     # Infinity Cache: rotate past this many bytes
+METRIC = "frames/sec (obs=8,pred=12) g2k_lstm_mcr train step; ADE/FDE vs reference"
 
 
+# ---------------------------------------------------------------------------
+# algorithmic bytes: compulsory HBM traffic of one launch
+# ---------------------------------------------------------------------------
 def algorithmic_bytes(b, H, params_bytes):
-    """Compulsory bytes one launch of g2k_step_fused_f32 moves:
-    reads pos/vislet/targets of ACTIVE pedestrians, G, h_in, n_active, weights;
-    writes pred (all Nmax columns, padding zero-filled), h_out, metrics."""
+    """One g2k_step_fused_f32 launch: reads the ACTIVE pedestrians' positions
+    (W rows), vislet and targets (F frames x 24 floats), G, h_in, n_active and
+    the weights; writes pred for the active columns (padded columns are not
+    written), h_out and the metrics row."""
     S, W, Nmax, _ = b.pos.shape
     F, L2, D, T = b.F, 24, 16, 8
     nact = b.n_active.astype(np.int64)
     rd = (W * nact * 8).sum() + (2 * nact * 4).sum() + S * D * T * 4 \
         + (F * nact * L2 * 4).sum() + S * D * H * 4 + S * 4 + params_bytes
-    wr = S * F * L2 * Nmax * 4 + S * D * H * 4 + S * 8 * 4
+    wr = (F * L2 * nact * 4).sum() + S * D * H * 4 + S * 8 * 4
     return int(rd + wr)
 
 
-def cpu_baseline(b, params_np, budget_s=12.0):
-    """The float64 oracle (oracle/g2k_ref.py) in the reference's loop
-    structure, one scene at a time, one thread, on a bounded sample."""
+def train_algorithmic_bytes(b, H, params_bytes, P):
+    """One train step (forward outputs + gradient + update): the forward's
+    bytes, the [P + 2] gradient written and read back, the parameters and the
+    RMSProp mean squares read and written once."""
+    return algorithmic_bytes(b, H, params_bytes) + 2 * (P + 2) * 4 + 4 * P * 4
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (BASELINE.md §2): the float64 oracle in the reference's loop
+# structure, on the GPU box's host cores, before the GPU is touched
+# ---------------------------------------------------------------------------
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _oracle_scenes(b, params_np, lo, hi, budget_s, threads):
+    """Scenes lo, lo+1, ... < hi through oracle.scene_step (one scene at a
+    time, the reference's per-batch loop) until budget_s has elapsed;
+    returns (frames, seconds)."""
     from threadpoolctl import threadpool_limits
     from oracle import g2k_ref as ref
     frames = 0
-    scenes = 0
-    with threadpool_limits(limits=1):
+    with threadpool_limits(limits=threads):
         t0 = time.perf_counter()
-        while scenes < b.S:
-            s = scenes
+        s = lo
+        while True:
             ref.scene_step(b.pos[s], b.vislet[s], b.G[s], params_np, b.targets[s],
                            b.n_active[s], b.h0[s], n_frames=b.F, stride=b.stride)
             frames += b.F
-            scenes += 1
+            s = s + 1 if s + 1 < hi else lo
             if time.perf_counter() - t0 > budget_s:
                 break
-        dt = time.perf_counter() - t0
-    return dict(value=frames / dt, unit="frames/s", cores=1, kind="port",
-                sample=f"{scenes} scenes x {b.F} frames of the same workload "
-                       f"(float64 NumPy oracle, 1 thread, {dt:.1f} s)")
+        return frames, time.perf_counter() - t0
 
 
-def time_train(args, params, t, dev, dist, S, F, world):
-    """--mode train (SURVEY.md §8(d)): the same step plus loss gradient, ONE
-    all-reduce of the flat [P + 2] gradient buffer across ranks (RCCL under
-    the nccl backend) and the RMSProp update (multimodaltraj_2_amd/train_step.py).
-    Timed like the reference-mode step: barrier + synchronize on both sides,
-    max over ranks."""
-    from multimodaltraj_2_amd.train_step import TrainStep
-    step = TrainStep(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
-    for _ in range(args.warmup):
-        step.run()
-    torch.cuda.synchronize()
+def _pool_worker(a):
+    cfg, seed, lo, hi, budget = a
+    c = CONFIGS[cfg]
+    b = make_batch(hi, c["Nmax"], c["H"], F=FRAMES_PER_SCENE, seed=seed)
+    p = fs.init_params(c["Nmax"], seed=0).numpy()
+    return _oracle_scenes(b, p, lo, hi, budget, 1)
+
+
+def cpu_baseline(cfg, b, params_np, budget_s, procs):
+    """Three denominators: one process with one BLAS thread
+    (how the reference runs: one Python process, tiny matrices), one process
+    with all BLAS threads, and the all-core aggregate (``procs`` processes on
+    disjoint scenes, spawned before this process touches the GPU)."""
+    import multiprocessing as mp
+    S = b.S
+    f1, t1 = _oracle_scenes(b, params_np, 0, S, budget_s, 1)
+    fa, ta = _oracle_scenes(b, params_np, 0, S, budget_s / 2, None)
+    per = max(1, S // procs)
+    jobs = [(cfg, 1, (i * per) % S, min(S, (i * per) % S + per), budget_s / 2)
+            for i in range(procs)]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_pool_worker, jobs)
+    agg = sum(f for f, _ in res) / max(t for _, t in res)
+    return {"value": f1 / t1, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"the float64 NumPy oracle (oracle/g2k_ref.py) in train.py's per-scene loop, "
+                      f"{f1 // b.F} scenes x {b.F} frames of the same workload in {t1:.1f} s, "
+                      f"1 thread (the reference's TF path cannot run here: no TF 1.x)",
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+            "blas_all_threads": {"value": fa / ta, "unit": "frames/s", "seconds": round(ta, 2)},
+            "all_core_aggregate": {"value": agg, "unit": "frames/s", "processes": procs,
+                                   "note": "disjoint scene slices, one BLAS thread each"}}
+
+
+# ---------------------------------------------------------------------------
+# multi-rank launcher (the parent never initialises the GPU)
+# ---------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args, argv):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------
+# timing
+# ---------------------------------------------------------------------------
+def timed(step, n, warmup, dist, sync):
+    """W untimed steps, then K steps bracketed by barrier + synchronize on
+    both sides; returns the max over ranks of the elapsed seconds."""
+    for i in range(warmup):
+        step(i)
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        g = step.run()
-    torch.cuda.synchronize()
+    for i in range(n):
+        step(i)
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     el = time.perf_counter() - t0
     if dist is not None:
-        e = torch.tensor([el], device=dev, dtype=torch.float64)
+        e = torch.tensor([el], dtype=torch.float64,
+                         device="cuda" if torch.cuda.is_initialized() else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         el = float(e.item())
-    gl = g.double().cpu().numpy()
-    return {"metric": "frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + L2 loss gradient + "
-                      "gradient all-reduce + RMSProp update",
-            "value": S * F * world * args.steps / el, "unit": "frames/s",
-            "ms_per_step": el / args.steps * 1e3, "allreduce_bytes": int(g.numel() * 4),
-            "loss_per_prediction_last_step": float(gl[-2] / max(gl[-1], 1.0)),
-            "optimizer": "RMSProp lr 0.005 decay 0.95, global-norm clip 10 (argParser.py:38-47)"}
+    return el
 
 
-def load_pmc(config):
-    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+def event_time(step, reps, stream):
+    """Average seconds per step from HIP events recorded on the stream the
+    kernels are launched on."""
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for i in range(reps):
+        step(i)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / 1e3 / reps
+
+
+def load_pmc(name):
+    p = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
     if not os.path.exists(p):
         return None
     try:
@@ -117,29 +212,53 @@ def load_pmc(config):
         return None
 
 
-def main():
+def selftest_worker(args, world, rank):
+    """--selftest-launcher (CPU, gloo): the launcher, the process-group check,
+    the timing brackets and the metric all-reduce, with a no-op step in place
+    of the HIP kernel (tests/test_bench_launcher.py)."""
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    if dist.get_world_size() != args.gpus:
+        raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    world = dist.get_world_size()
+    metrics = torch.full((4, 8), float(rank + 1), dtype=torch.float64)
+    el = timed(lambda i: None, args.steps, args.warmup, dist, lambda: None)
+    tot = metrics.sum(dim=0)
+    dist.all_reduce(tot)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "selftest": True, "elapsed_s": el,
+                          "metric_sums": tot.tolist()}), flush=True)
+    dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="eth_hotel_synth", choices=sorted(CONFIGS))
     ap.add_argument("--scenes", type=int, default=0, help="override scenes per rank")
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="input batches to rotate over (0: enough to exceed the 256 MiB MALL)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--no-train", action="store_true", help="skip the --mode train timing")
-    args = ap.parse_args()
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="processes of the all-core CPU aggregate (0: min(16, cpu_count))")
+    ap.add_argument("--no-train", action="store_true", help="skip the train-mode timing")
+    ap.add_argument("--selftest-launcher", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args(argv)
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.selftest_launcher:
+        return selftest_worker(args, world, rank)
 
     cfg = dict(CONFIGS[args.config])
     if args.config in ("eth_ucy_loo_kfold4", "dense_crowd"):
@@ -147,68 +266,68 @@ def main():
     S = args.scenes or cfg["S"]
     Nmax, H, F = cfg["Nmax"], cfg["H"], FRAMES_PER_SCENE
     b = make_batch(S, Nmax, H, F=F, seed=1 + rank)
-    params = fs.init_params(Nmax, seed=0, device=dev)
-    t = b.to_device(dev)
-    out = fs.StepOutputs(pred=torch.empty((S, F, 24, Nmax), device=dev),
-                         h=torch.empty((S, 16, H), device=dev),
-                         metrics=torch.empty((S, 8), device=dev))
+    params_host = fs.init_params(Nmax, seed=0)
 
-    # one validated launch bound to the resident buffers; each step is one C call
-    plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
-                       t["h0"], out=out)
-    step = plan.run
+    # CPU baseline first: its worker processes are spawned before this
+    # process initialises the GPU
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(args.config, b, params_host.numpy(), args.cpu_budget, procs)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    # reference mode: replicas only; the ADE/FDE numerators are summed across
-    # ranks once at the end, outside the timed region
-    tot = out.metrics.double().sum(dim=0)
-    if dist is not None:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-        dist.all_reduce(tot)
-
-    # dominant-kernel duration: HIP events on the stream the kernel runs on
-    stream = torch.cuda.current_stream()
-    reps = max(20, min(args.steps, 200))
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(reps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    kern_s = ev0.elapsed_time(ev1) / 1e3 / reps
-
-    frames_total = S * F * world
-    value = frames_total * args.steps / elapsed
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    params = params_host.to(dev)
     pbytes = sum(getattr(params, k).numel() * 4 for k in ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo"))
     abytes = algorithmic_bytes(b, H, pbytes)
-    achieved = abytes / kern_s / 1e9
-    pmc = load_pmc(args.config)
+    K = args.rotate or max(1, -(-MALL_BYTES // abytes) + 1)
 
-    train = None if args.no_train else time_train(args, params, t, dev, dist, S, F, world)
+    # K device-resident input batches (the base batch plus small per-batch
+    # position offsets, so no two share a cache line) and their plans
+    base = b.to_device(dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    batches, plans = [], []
+    for k in range(K):
+        t = {key: (v.clone() if isinstance(v, torch.Tensor) else v) for key, v in base.items()}
+        if k:
+            t["pos"].add_(1e-3 * torch.randn(t["pos"].shape, device=dev, generator=gen))
+            t["targets"].add_(1e-3 * torch.randn(t["targets"].shape, device=dev, generator=gen))
+        out = fs.StepOutputs(pred=torch.zeros((S, F, 24, Nmax), device=dev),
+                             h=torch.empty((S, 16, H), device=dev),
+                             metrics=torch.empty((S, 8), device=dev))
+        batches.append(t)
+        plans.append(fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"],
+                                 t["n_active"], t["h0"], out=out))
+
+    def step(i):
+        plans[i % K].run()
+
+    elapsed = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    # reference mode: replicas only; the ADE/FDE numerators of the last batch
+    # are summed across ranks once at the end
+    tot = plans[(args.steps - 1) % K].out.metrics.double().sum(dim=0)
+    if dist is not None:
+        dist.all_reduce(tot)
+    stream = torch.cuda.current_stream()
+    kern_s = event_time(step, max(20, min(args.steps, 200)), stream)
+    achieved = abytes / kern_s / 1e9
+
+    train = None
+    if not args.no_train:
+        train = time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K)
 
     if rank == 0:
-        cpu = None if args.no_cpu_baseline or world > 1 else \
-            cpu_baseline(b, params.numpy(), budget_s=args.cpu_budget)
-        m = tot.double().cpu().numpy()
+        m = tot.cpu().numpy()
         line = {
-            "metric": "frames/sec (obs=8,pred=12) g2k_lstm_mcr train step; ADE/FDE vs reference",
-            "value": value,
+            "metric": METRIC,
+            "value": S * F * world * args.steps / elapsed,
             "unit": "frames/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -219,22 +338,66 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded random-walk ETH-shaped scenes; N(0,1) weights)",
+            "mode": "reference (train.py:197-276: forward, recurrence, ADE/FDE; the reference "
+                    "has no backward)",
             "config": {"workload": args.config, "scenes_per_gpu": S, "global_scenes": S * world,
                        "frames_per_scene": F, "obs_len": 8, "pred_len": 12, "Nmax": Nmax,
-                       "hidden": H, "D": 16, "parallelism": f"dp{world}"},
+                       "hidden": H, "D": 16, "parallelism": f"dp{world}",
+                       "input_batches_rotated": K},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc, "kernel": "g2k_step_fused_f32 (g2k_scene_kernel)",
+                         "traffic": load_pmc(args.config),
+                         "kernel": "g2k_step_fused_f32 (g2k_scene_kernel)",
                          "kernel_us": kern_s * 1e6, "algorithmic_bytes": abytes},
             "cpu_baseline": cpu,
             "ade_fde_all_ranks": {"ADE": float(m[0] / max(m[1], 1)),
                                   "FDE_frob_per_frame": float(np.sqrt(m[2]) / max(m[5], 1))},
             "train_mode": train,
         }
-        print(json.dumps(line))
+        if cpu:
+            v = line["value"]
+            line["speedup_vs_cpu"] = {"one_thread": v / cpu["value"],
+                                      "blas_all_threads": v / cpu["blas_all_threads"]["value"],
+                                      "all_core_aggregate": v / cpu["all_core_aggregate"]["value"]}
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
+
+
+def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K):
+    """--mode train (SURVEY.md §8(d)): the same step plus loss gradient, ONE
+    all-reduce of the flat [P + 2] gradient buffer across ranks (RCCL under
+    the nccl backend) and the RMSProp update (multimodaltraj_2_amd/train_step.py).
+    Timed like the reference-mode step over the same rotated batches."""
+    from multimodaltraj_2_amd.train_step import TrainStep
+    t0 = batches[0]
+    ts = TrainStep(params, t0["pos"], t0["vislet"], t0["G"], t0["targets"], t0["n_active"],
+                   t0["h0"])
+    for t in batches[1:]:
+        ts.bind(t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+    last = {}
+
+    def step(i):
+        last["g"] = ts.run(i % K)
+
+    el = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    gl = last["g"].double().cpu().numpy()
+    kern_s = event_time(step, max(20, min(args.steps, 200)), torch.cuda.current_stream())
+    abytes = train_algorithmic_bytes(b, H, pbytes, ts.P)
+    achieved = abytes / kern_s / 1e9
+    return {"metric": "frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + L2 loss gradient + "
+                      "gradient all-reduce + RMSProp update",
+            "value": S * F * world * args.steps / el, "unit": "frames/s",
+            "ms_per_step": el / args.steps * 1e3, "allreduce_bytes": int((ts.P + 2) * 4),
+            "loss_per_prediction_last_step": float(gl[-2] / max(gl[-1], 1.0)),
+            "optimizer": "RMSProp lr 0.005 decay 0.95, global-norm clip 10 (argParser.py:38-47)",
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": load_pmc(args.config + "_train"),
+                         "kernel": ts.kernel_names, "step_us": kern_s * 1e6,
+                         "algorithmic_bytes": abytes}}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

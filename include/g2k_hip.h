@@ -16,9 +16,12 @@
  *   - return 0 on success, a negative G2K_E* code on failure; the message of
  *     the last failure on this thread is in g2k_last_error();
  *   - deterministic: fixed reduction order, no float atomics;
- *   - fixed model geometry: T (obs_len) = 8, L (pred_len) = 12, D = 16
- *     (= neighborhood_size / grid_size, train.py:93); H a multiple of 64 in
- *     [64, 512]; Nmax in [1, 256].
+ *   - fixed model geometry: T (obs_len) = 8, L (pred_len) = 12; D = 16
+ *     (= neighborhood_size / grid_size, train.py:93) for the fused step and
+ *     train mode, D in 1..16 for g2k_mcr_forward_f32 / g2k_frame_recurrence_f32
+ *     / g2k_ade_fde_f32 (sample.py runs D = num_freq_blocks = 10,
+ *     sample.py:168-205, and the reference checkpoints are D = 10);
+ *     H in {64, 128, 256, 512}; Nmax in [1, 256].
  */
 #ifndef G2K_HIP_H
 #define G2K_HIP_H
@@ -29,7 +32,7 @@
 extern "C" {
 #endif
 
-#define G2K_ABI_VERSION 1
+#define G2K_ABI_VERSION 2
 
 enum {
   G2K_OK = 0,
@@ -66,12 +69,11 @@ typedef struct g2k_weights {
 int g2k_abi_version(void);
 const char* g2k_last_error(void);
 
-/* Bytes of dynamic LDS per g2k_frames_kernel workgroup for `d` (0 if unsupported). */
+/* Bytes of dynamic LDS per g2k_step_fused_f32 workgroup for `d` (0 if unsupported). */
 int64_t g2k_step_lds_bytes(const g2k_dims* d);
 
 /* Bytes of caller-provided device workspace g2k_step_fused_f32 needs for `d`
- * (attention weights [S, F, D, D] + per-chunk ADE/FDE partial sums); -1 on
- * invalid dims.  The workspace must be 16-byte aligned. */
+ * (0: every intermediate stays on chip); -1 on invalid dims. */
 int64_t g2k_step_workspace_bytes(const g2k_dims* d);
 
 /*
@@ -87,8 +89,7 @@ int64_t g2k_step_workspace_bytes(const g2k_dims* d);
  * frame) and its per-batch setup train.py:178-195.
  * One launch of the wave-specialised scene kernel (one workgroup per scene:
  * producer waves run a2-a7 / a9 per frame, recurrence waves run a8, LDS flags
- * between them).  G2K_STEP_SPLIT=1 selects the older two-launch split
- * (frame-parallel kernel + recurrence kernel, As handed over in `workspace`).
+ * between them).
  *
  *   pos      [S, W, Nmax, 2]       pedestrian (x, y) rows
  *   vislet   [S, 2, Nmax]          load_traj.py:139 rows 4:6 slice
@@ -99,13 +100,15 @@ int64_t g2k_step_workspace_bytes(const g2k_dims* d);
  *   ped_mask [S, Nmax] uint8 or NULL  rows with a target; NULL = all active
  *   h_in     [S, D, H]             hidden_state entering frame 0
  *   h_out    [S, D, H]             hidden_state after the last frame (may alias h_in)
- *   pred     [S, F, 2L, Nmax]      pred_path_band per frame (rows x then y)
+ *   pred     [S, F, 2L, Nmax]      pred_path_band per frame (rows x then y); only
+ *                                  frames < n_frames and columns < n_active (in
+ *                                  groups of 4, the extra columns 0) are written
  *   metrics  [S, 8]                {sum ade_spec, count, sum |fde|^2,
  *                                   sum ade_l2, sum |fde|, frames, 0, 0}
  *   A_out    [S, F, D, D] or NULL  krnl_mdl.attn per frame (frames < n_frames)
  *   cost_out [S, F, T, T] or NULL  krnl_mdl.cost per frame (frames < n_frames)
  *   lambda                          lambda_param (argParser.py, 5e-4)
- *   workspace, workspace_bytes      >= g2k_step_workspace_bytes(d)
+ *   workspace, workspace_bytes      >= g2k_step_workspace_bytes(d) (may be NULL / 0)
  * h_out must not alias h_in across scenes being read (same-scene aliasing is fine).
  */
 int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w,
@@ -220,7 +223,23 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
                       int64_t workspace_bytes, void* stream);
 int g2k_update_f32(float* params, float* ms, const float* grad, int64_t n_params, float lr,
                    float decay, float grad_clip, void* stream);
+int64_t g2k_train_workspace_bytes(const g2k_dims* d);
+int g2k_train_step_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
+                       const float* vislet, const float* G, const float* targets,
+                       const int32_t* n_active, const int32_t* n_frames,
+                       const uint8_t* ped_mask, const float* h_in, float* h_out, float* pred,
+                       float* metrics, float lambda, float* grad, void* workspace,
+                       int64_t workspace_bytes, float* params, float* ms, float lr, float decay,
+                       float grad_clip, void* stream);
 /*
+ * g2k_train_step_f32: one train-mode step in one call: the fused step's
+ *   outputs (h_out, pred, metrics as g2k_step_fused_f32) AND grad [P + 2] from
+ *   the same launch (the producers turn each prediction tile's error into the
+ *   loss gradient; nothing is recomputed), then the per-scene gradient rows
+ *   summed in a fixed order; with params != NULL (one rank) also the update
+ *   of g2k_update_f32 (ms NULL: SGD).  Across ranks: call with params NULL,
+ *   all-reduce grad, then g2k_update_f32.  workspace >=
+ *   g2k_train_workspace_bytes(d) (one gradient row per scene).
  * g2k_step_grad_update_f32: one rank's whole train-mode update (nothing to
  *   all-reduce): g2k_step_grad_f32 then g2k_update_f32 on params [P] (the flat
  *   buffer in g2k_weights order, P = g2k_grad_size) with the last reduction

@@ -56,12 +56,17 @@ SYMBOLS = {
     "g2k_step_grad_update_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
                                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp,
                                          c_vp, c_i64, c_vp, c_vp, c_f32, c_f32, c_f32, c_vp]),
+    "g2k_train_workspace_bytes": (c_i64, [ctypes.POINTER(G2KDims)]),
+    "g2k_train_step_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
+                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                   c_vp, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp, c_f32, c_f32,
+                                   c_f32, c_vp]),
     "g2k_context_conv_workspace_bytes": (c_i64, [c_i32, c_i32, c_i32]),
     "g2k_context_conv_f32": (c_int, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp,
                                      c_vp, c_i64, c_vp]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class G2KLibraryError(RuntimeError):
@@ -87,8 +92,7 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    # G2K_LIB_PATH: A/B tooling only (tools/ab), never set by tests / bench defaults
-    p = path or os.environ.get("G2K_LIB_PATH") or LIB_PATH
+    p = path or LIB_PATH
     if not os.path.exists(p):
         raise G2KLibraryError(
             f"{p} not found: the HIP library is not built (run `python __graft_entry__.py`); "

@@ -1,16 +1,24 @@
-"""Compile libg2k_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+"""Compile libg2k_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+
+Each csrc/*.hip translation unit is compiled to an object in parallel, then
+linked into one shared library (no device code crosses translation units)."""
 from __future__ import annotations
 
+import glob
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = [os.path.join(HERE, "csrc", "g2k_kernels.hip")]
+CSRC = os.path.join(HERE, "csrc")
+SRC = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+HDR = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "g2k_hip.h")]
 OUT = os.path.join(HERE, "libg2k_hip.so")
+OBJ = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-fno-slp-vectorize", "-std=c++17", "-shared", "-fPIC",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fno-slp-vectorize", "-std=c++17", "-fPIC",
          "-I" + os.path.join(ROOT, "include")]
 
 
@@ -18,13 +26,24 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SRC + [os.path.join(ROOT, "include", "g2k_hip.h")]
-    return any(os.path.getmtime(p) > t for p in deps)
+    return any(os.path.getmtime(p) > t for p in SRC + HDR)
+
+
+def _compile(src, verbose):
+    obj = os.path.join(OBJ, os.path.basename(src)[:-4] + ".o")
+    cmd = [HIPCC, *FLAGS, "-c", "-o", obj, src]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return obj
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
     if force or needs_build():
-        cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *SRC]
+        os.makedirs(OBJ, exist_ok=True)
+        with ThreadPoolExecutor(max_workers=min(8, len(SRC))) as ex:
+            objs = list(ex.map(lambda s: _compile(s, verbose), SRC))
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

@@ -1,0 +1,1146 @@
+// g2k_scene.hip — the fused per-frame step (train.py:197-276 over S scenes x
+// F frames) in ONE launch, and its train mode: the same launch also forms
+// the scene's loss gradient (SURVEY.md §8(d) "--mode train").
+//
+// g2k_scene_kernel<TPW, NP, GRAD>: one workgroup per scene, wave-specialised.
+// Waves 0..3 (one per SIMD) run the frame-sequential recurrence (a8,
+// Recur::step_seq, h in MFMA registers); waves 4..4+NP-1 are producers that
+// run the frame-parallel body: frame heads (a2-a7: window norms, embeddings,
+// E, A, As, M = Wc @ cost) into LDS rings with per-frame flags, then the
+// prediction tiles (Y = M @ Wo, pred_path_band) with the a9 error terms.  The
+// two roles never share a barrier inside a chunk of frames: the recurrence's
+// latency chain runs while the producers stream predictions, targets and
+// errors, and As never leaves the CU.
+//
+// GRAD (train mode): each producer owns whole frames (fl = pw, pw + NP, ...)
+// and, per 16-pedestrian tile, turns the prediction error into dY (masked),
+// dM_f += dY @ Wo^T and dWo^T += dY^T @ M_f; after its frame's tiles it forms
+// the frame's weight-side terms (dcost = Wc^T dM, dE = lambda dcost G^T,
+// dWc_f = dM cost^T, dK1_f = dE Uaug^T, dUaug_f = K1^T dE) and adds them into
+// the scene's accumulators in frame order (an LDS sequence word: the same
+// sums in the same order whatever the timing -> deterministic, no atomics on
+// data).  After the last frame the producers expand the accumulators into
+// the scene's gradient row [P + 2] (Wi through the window norms, Wii / Wv
+// through K1 = Wv[:, :16] Wii) — no recomputed forward, no second read of the
+// inputs except the position rows for dWi.  The rows are summed over scenes
+// by g2k_grad_rows_kernel (g2k_train.hip) in a fixed order.
+#include "g2k_common.h"
+#include "g2k_recur.h"
+
+namespace g2k {
+namespace {
+
+constexpr int kSceneChunk = 32;
+constexpr int kRecW = 4;
+// small block of weights / per-scene matrices in LDS (floats)
+constexpr int SM_WII = 0;     // [16][8]
+constexpr int SM_WV = 128;    // [8][18]
+constexpr int SM_BV = 272;    // [16]
+constexpr int SM_WR = 288;    // [8][2]
+constexpr int SM_WC = 304;    // [24][8]
+constexpr int SM_G = 496;     // [16][8]  G (lambda applied at use)
+// weight-derived matrices (frame head): K1 = [Wv16 @ Wii | Wv[:,16] | Wv[:,17] | 1 | 0]
+// ([8][12]), K2 = Wc @ K1 ([24][12])
+constexpr int SM_K1 = 640;
+constexpr int SM_K2 = 752;
+constexpr int kSceneSmall = 1088;
+constexpr int kKA = 12;       // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
+// train mode
+constexpr int kGFrame = 832;  // per-producer frame scratch: dM [24][8], dcost [8][8], dE [8][16],
+                              // terms: dWc_f [24][8], dK1_f [8][10], dUaug_f [11][16]
+constexpr int kGT_DM = 0, kGT_DC = 192, kGT_DE = 256, kGT_TERMS = 384, kGTerms = 448;
+constexpr int kGAccFixed = 320;   // dWc [24][8], dK1 [8][10], dVe [2][16], dbv [16]
+constexpr int kGA_WC = 0, kGA_K1 = 192, kGA_VE = 272, kGA_BV = 304;
+
+struct SceneLayout {
+  int fc, wcmax, pp;   // frames per chunk, window rows per chunk, pos row pitch (floats)
+  int o_wi, o_wo, o_vis, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_mflag, o_red, o_pos,
+      o_vg;
+  // train mode (zero-sized otherwise)
+  int wtot;            // window rows of the whole scene ((F - 1) * stride + T)
+  int dwo_seq;         // 1: dWo^T accumulated in frame order (one copy); 0: one copy per producer
+  int o_cost, o_gframe, o_gacc, o_gdv, o_gdwo, o_gseq;
+  int total;           // floats
+};
+
+__host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int F, int fc, int NP,
+                                                       bool grad) {
+  SceneLayout s;
+  s.fc = fc;
+  s.wcmax = (fc - 1) * stride + kT;
+  s.pp = 2 * Nmax + 4;                        // padded rows: lanes reading across rows spread banks
+  int o = 0;
+  s.o_wi = o;    o += rup4(Nmax * kD);
+  s.o_wo = o;    o += rup4(kT * Nmax);
+  s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
+  s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
+  s.o_small = o; o += kSceneSmall;
+  s.o_y = o;     o += NP * kD * kL2;                  // tile transpose scratch (Y, then dY)
+  s.o_met = o;   o += NP * 8;
+  s.o_ring = o;  o += fc * kD * kD;
+  s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
+  s.o_flag = o;  o += rup4(fc);                      // As ring flags (recurrence polls)
+  s.o_mflag = o; o += rup4(fc);                      // M ring flags (prediction tiles poll)
+  s.o_red = o;   o += 4 * 16 * kRecW;
+  s.o_pos = o;   o += s.wcmax * s.pp;                  // raw position window (LDS-DMA)
+  s.o_vg = o;    o += rup4((s.wcmax + 3) * kT);       // VG = V @ g: window, Ve0, Ve1, bv rows
+  s.wtot = (F > 0 ? F - 1 : 0) * stride + kT;
+  s.dwo_seq = (int64_t)NP * Nmax * kT * 4 > 32 * 1024 ? 1 : 0;
+  s.o_cost = s.o_gframe = s.o_gacc = s.o_gdv = s.o_gdwo = s.o_gseq = o;
+  if (grad) {
+    s.o_cost = o;   o += fc * kT * kT;                 // cost_f per chunk frame (head -> terms)
+    s.o_gframe = o; o += NP * kGFrame;
+    s.o_gacc = o;   o += kGAccFixed;
+    s.o_gdv = o;    o += rup4(s.wtot * kD);            // dV: window-row gradient [wtot][16]
+    s.o_gdwo = o;   o += (s.dwo_seq ? 1 : NP) * Nmax * kT;   // dWo^T [Nmax][8]
+    s.o_gseq = o;   o += rup4(2 + (Nmax + 15) / 16);   // frame seq, done count, tile seqs
+  }
+  s.total = o;
+  return s;
+}
+
+__host__ inline SceneLayout scene_layout(const g2k_dims* d, int NP, bool grad) {
+  int fc = d->F < 1 ? 1 : (d->F < kSceneChunk ? d->F : kSceneChunk);
+  SceneLayout l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad);
+  while ((int64_t)l.total * 4 > 160 * 1024 && fc > 1) {
+    fc = (fc + 1) / 2;
+    l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad);
+  }
+  return l;
+}
+
+// frame head output: the x / y row tiles of M^T
+struct FrameHeadOut {
+  f32x4 mT0, mT1;   // M[L][4q+i] (x rows), M[12+L][4q+i] (y rows)
+};
+
+// Partner lane's value across lane groups (q ^ 1 by permlane16, q ^ 2 by
+// permlane32): of the pair a swap returns, one element is this lane's own
+// value, the other the partner's.
+__device__ __forceinline__ float partner16(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return a[0] == __float_as_uint(v) ? __uint_as_float(a[1]) : __uint_as_float(a[0]);
+}
+__device__ __forceinline__ float partner32(float v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return a[0] == __float_as_uint(v) ? __uint_as_float(a[1]) : __uint_as_float(a[0]);
+}
+
+// As = softmax(exp(A) / cumsum(exp(A), axis 0), axis -1)  (train.py:240) of
+// one frame's A in the MFMA result layout (column L, rows 4q + i), written
+// to as_dst [16][16].  The ratio exp(A_r) / sum_{k<=r} exp(A_k) is invariant
+// to a per-column shift: with the column max M, e = exp(A - M) lies in (0, 1]
+// and the prefix sums (in-lane, then across lane groups by permlane swaps)
+// cannot overflow.  If a prefix sum underflows (the column's leading rows are
+// ~87 below its max) the wave redoes the column with a running (max, sum)
+// pair, which is exact for any finite A.  Then a 16-lane row softmax of
+// values in (0, 1].  Stored as As * log2(e): the recurrence's A operand.
+__device__ __forceinline__ void attn_weights(const f32x4 aA, float* as_dst, int L, int q) {
+  float mx = fmaxf(fmaxf(aA[0], aA[1]), fmaxf(aA[2], aA[3]));
+  mx = fmaxf(mx, partner16(mx));
+  mx = fmaxf(mx, partner32(mx));
+  float e[4], p[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = __expf(aA[i] - mx);
+  p[0] = e[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) p[i] = p[i - 1] + e[i];
+  const float t1 = partner16(p[3]), t2 = partner32(p[3]), t3 = partner32(t1);
+  const float pre = ((q & 2) ? t2 + t3 : 0.f) + ((q & 1) ? t1 : 0.f);   // groups before q
+  float R[4];
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float P = pre + p[i];
+    bad |= !(P >= 1e-30f);
+    R[i] = e[i] * rcp(P);
+  }
+  if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+    // running (max, sum exp) down the rows; exclusive prefix over the groups
+    float m_i[4], s_i[4];
+    float m = aA[0], sacc = 1.0f;
+    m_i[0] = m; s_i[0] = sacc;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      lse_combine(m, sacc, aA[i], 1.0f);
+      m_i[i] = m; s_i[i] = sacc;
+    }
+    const float m1 = partner16(m), s1 = partner16(sacc);
+    const float m2 = partner32(m), s2 = partner32(sacc);
+    const float m3 = partner32(m1), s3 = partner32(s1);
+    float pm = m2, ps = s2;
+    lse_combine(pm, ps, m3, s3);
+    float mp = -INFINITY, sp = 0.f;
+    if (q & 2) { mp = pm; sp = ps; }
+    if (q & 1) {
+      if (q & 2) lse_combine(mp, sp, m1, s1);
+      else { mp = m1; sp = s1; }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float mr = m_i[i], sr = s_i[i];
+      if (q > 0) lse_combine(mr, sr, mp, sp);
+      R[i] = __expf(aA[i] - mr) * rcp(sr);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float ex = __expf(R[i]);
+    as_dst[(4 * q + i) * kD + L] = ex * (rcp(row16_sum(ex)) * kLog2e);
+  }
+}
+
+// frame head: the g2k_lstm_mcr forward of one frame up to M (models/
+// g2k_lstm_mcr.py:99-124 with train.py:178-195), reassociated around the
+// weight-derived K1 / K2 (computed once per workgroup in scene_stage):
+//   E    = K1 @ Uaug      Uaug = [U (8 window rows of V); Ve0; Ve1; bv; 0]
+//        = Wv[:, :16] @ (Wii @ U) + Wv[:, 16:18] @ Ve + bv          (:105, 112)
+//   A    = g @ (E * Rm)                                             (:105-106)
+//   cost = E @ g = K1 @ VGaug        (VGaug = Uaug @ g, rows of VG)  (:112-113)
+//   M    = Wc @ cost = K2 @ VGaug                                   (:119)
+// Contractions over the 12 augmented rows use k = 4 ks + q (3 k-steps);
+// A contracts over t = 4q + ks (rows of E as the MFMA left them).  As goes
+// to `as_dst`; cost to `cost_g` (global, krnl_mdl.cost) and / or `cost_l`
+// (LDS, train mode); the x / y row tiles of M^T are returned (M[L][4q+i]).
+__device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float* sV,
+                                                   const float* sVG, int wrow0, int wcmax,
+                                                   const float (&rm)[4], float lam, float* as_dst,
+                                                   float* A_g, float* cost_g, float* cost_l, int L,
+                                                   int q) {
+  float ka[3], ua[3], va[3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const int k = 4 * ks + q;
+    ka[ks] = L < kT ? sm[SM_K1 + L * kKA + k] : 0.f;
+    if (ks < 2) {
+      ua[ks] = sV[(wrow0 + k) * kD + L];
+      va[ks] = L < kT ? sVG[(wrow0 + k) * kT + L] : 0.f;
+    } else {
+      ua[ks] = q < 2 ? sV[(wcmax + q) * kD + L] : (q == 2 ? sm[SM_BV + L] : 0.f);
+      va[ks] = L >= kT || q == 3 ? 0.f : sVG[(wcmax + q) * kT + L];   // Ve0, Ve1, bv rows
+    }
+  }
+  f32x4 eN = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);          // E[4q+i][L]
+  FrameHeadOut o;
+  o.mT0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  o.mT1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const int k = 4 * ks + q;
+    const float bx = L < kL ? sm[SM_K2 + L * kKA + k] : 0.f;
+    const float by = L < kL ? sm[SM_K2 + (kL + L) * kKA + k] : 0.f;
+    o.mT0 = mfma4(va[ks], bx, o.mT0);   // M[L][4q+i]       (x rows)
+    o.mT1 = mfma4(va[ks], by, o.mT1);   // M[12+L][4q+i]    (y rows)
+  }
+  f32x4 aA = {0.f, 0.f, 0.f, 0.f};
+  {
+    float em[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) em[i] = eN[i] * rm[i];                    // rm = 0 for t >= 8
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const float gA = q < 2 ? lam * sm[SM_G + L * kT + 4 * q + ks] : 0.f;  // g[r = L][t]
+      aA = mfma4(gA, em[ks], aA);                                        // A[4q+i][L]
+    }
+  }
+  if (A_g) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) A_g[(4 * q + i) * kD + L] = aA[i];
+  }
+  if (cost_g || cost_l) {
+    f32x4 cC = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) cC = mfma4(ka[ks], va[ks], cC);      // cost[4q+i][L]
+    if (q < 2 && L < kT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (cost_g) cost_g[(4 * q + i) * kT + L] = cC[i];
+        if (cost_l) cost_l[(4 * q + i) * kT + L] = cC[i];
+      }
+    }
+  }
+  attn_weights(aA, as_dst, L, q);
+  return o;
+}
+
+// Per-workgroup context of the scene kernel (LDS carve-up, scene scalars).
+struct SceneCtx {
+  float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sPos, *sVG, *sY;
+  float *sCost, *sGFrame, *sGAcc, *sGdV, *sGdWo;
+  int* sFlag;     // As ring: global frame + 1 once the frame's As is in its slot
+  int* sMflag;    // M ring: global frame + 1 once the frame's M is in its slot
+  int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
+  int* sGseq;     // train: [0] frames added, [1] unused, [2 + t] frames added to dWo tile t
+  int s, tid, lane, wv, L, q, nact, nf, ntiles, ntact;
+};
+
+// LDS-DMA of a chunk's position window rows (train.py:76-79 window) into
+// rows of pitch lay.pp: wave w issues rows w, w + waves, ...
+template <int NT>
+__device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneLayout& lay,
+                                              const SceneCtx& c, int fb, int cnt) {
+  const int Nmax = a.d.Nmax, stride = a.d.stride;
+  const int wcc = (cnt - 1) * stride + kT;
+  const float* src = a.pos + ((size_t)c.s * a.d.W + fb * stride) * Nmax * 2;
+  const bool wide = (Nmax & 1) == 0 && (((uintptr_t)a.pos) & 15) == 0;
+  for (int r = c.wv; r < wcc; r += NT / 64) {
+    const float* g = src + (size_t)r * Nmax * 2;
+    float* d = c.sPos + r * lay.pp;
+    if (wide) {
+      for (int i = 0; i < Nmax / 2; i += 64)
+        if (i + c.lane < Nmax / 2) dma16(g + 4 * (i + c.lane), d + 4 * i);
+    } else {
+      for (int i = 0; i < 2 * Nmax; i += 64)
+        if (i + c.lane < 2 * Nmax)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + i + c.lane),
+                                           (__attribute__((address_space(3))) void*)(d + i), 4, 0, 0);
+    }
+  }
+}
+
+// One 16-row tile of the chunk's embedding rows, by MFMA (train.py:76-79,
+// 167-195): local rows r = w0 + L are the window rows (r < wcc: norms
+// ||pos||, formed here from the LDS window), the two vislet rows and a bv
+// pseudo-row (VG only).  V^T = Wi^T @ N^T over n (k = 4 ks + q), then
+// VG^T = (lambda G)^T @ V^T over d with V^T straight from the registers.
+// Lane (L, q) ends with V[r][4q..4q+3] and VG[r][4q..4q+3] (q < 2).
+__device__ __forceinline__ void scene_vtile(const StepArgs& a, const SceneLayout& lay,
+                                            const SceneCtx& c, int w0, int wcc) {
+  // branch-free: every lane loads at clamped addresses and selects, so the
+  // LDS reads of several k-steps are in flight together
+  const int Nmax = a.d.Nmax, L = c.L, q = c.q, nact = c.nact;
+  const int r = w0 + L;
+  const bool win = r < wcc, vis = r >= wcc && r < wcc + 2, bvrow = r == wcc + 2;
+  const float* prow = c.sPos + (win ? r : 0) * lay.pp;
+  const float* vrow = c.sVis + (vis ? r - wcc : 0) * Nmax;
+  struct Raw { float wi, px, py, v; };
+  auto load = [&](int ks) {
+    const int n = 4 * ks + q;
+    const int nc = n < Nmax ? n : Nmax - 1;
+    const float2 p = *reinterpret_cast<const float2*>(prow + 2 * nc);
+    return Raw{c.sWi[nc * kD + L], p.x, p.y, vrow[nc]};           // Wi[n][d = L], pos, vislet
+  };
+  auto value = [&](int ks, const Raw& w) {                         // N[w0 + L][n]
+    const int n = 4 * ks + q;
+    const float nrm = __builtin_amdgcn_sqrtf(fmaf(w.px, w.px, w.py * w.py));
+    return n < nact ? (win ? nrm : (vis ? w.v : 0.f)) : 0.f;
+  };
+  const int nks = (nact + 3) / 4;                                  // n >= nact contribute 0
+  f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+  int ks = 0;
+  for (; ks + 4 <= nks; ks += 4) {
+    Raw r0 = load(ks), r1 = load(ks + 1), r2 = load(ks + 2), r3 = load(ks + 3);
+    // keep all twelve loads unconditional and in flight together
+    asm volatile("" : "+v"(r0.wi), "+v"(r0.px), "+v"(r0.py), "+v"(r0.v), "+v"(r1.wi), "+v"(r1.px),
+                 "+v"(r1.py), "+v"(r1.v), "+v"(r2.wi), "+v"(r2.px), "+v"(r2.py), "+v"(r2.v),
+                 "+v"(r3.wi), "+v"(r3.px), "+v"(r3.py), "+v"(r3.v));
+    v0 = mfma4(r0.wi, value(ks, r0), v0);                          // V[w0 + L][4q + i]
+    v1 = mfma4(r1.wi, value(ks + 1, r1), v1);
+    v0 = mfma4(r2.wi, value(ks + 2, r2), v0);
+    v1 = mfma4(r3.wi, value(ks + 3, r3), v1);
+  }
+  for (; ks < nks; ++ks) {
+    Raw r0 = load(ks);
+    asm volatile("" : "+v"(r0.wi), "+v"(r0.px), "+v"(r0.py), "+v"(r0.v));
+    v0 = mfma4(r0.wi, value(ks, r0), v0);
+  }
+  f32x4 vt;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) vt[i] = v0[i] + v1[i];
+  f32x4 vg = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks2 = 0; ks2 < 4; ++ks2) {
+    const float gl = c.sm[SM_G + (4 * q + ks2) * kT + (L & 7)];
+    const float ga = L < kT ? a.lambda * gl : 0.f;                          // g[d][t2 = L]
+    const float bvv = c.sm[SM_BV + 4 * q + ks2];
+    vg = mfma4(ga, bvrow ? bvv : vt[ks2], vg);                             // VG[w0 + L][4q + i]
+  }
+  const int row = win ? r : lay.wcmax + (r - wcc);               // storage row
+  if (win || vis)
+    *reinterpret_cast<float4*>(c.sV + row * kD + 4 * q) = make_float4(vt[0], vt[1], vt[2], vt[3]);
+  if ((win || vis || bvrow) && q < 2)
+    *reinterpret_cast<float4*>(c.sVG + row * kT + 4 * q) = make_float4(vg[0], vg[1], vg[2], vg[3]);
+}
+
+// K1 = [Wv[:, :16] @ Wii | Wv[:, 16] | Wv[:, 17] | 1 | 0] ([8][12]) and
+// K2 = Wc @ K1 ([24][12]) by MFMA in one wave (weights only; see frame_head).
+__device__ __forceinline__ void scene_kmats(const SceneCtx& c) {
+  const int L = c.L, q = c.q, L7 = L & 7;
+  const float* sm = c.sm;
+  float av[4], bw[4];
+  float wv16[4], wv17[4], wc0[4], wc1[4];
+  const int q1 = q & 1;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int d = 4 * q + ks;
+    av[ks] = sm[SM_WV + L7 * (kD + 2) + d];                      // Wv[t = L][d]
+    bw[ks] = sm[SM_WII + d * kT + L7];                           // Wii[d][k = L]
+    const int t = 4 * q1 + ks;
+    wv16[ks] = sm[SM_WV + t * (kD + 2) + kD];
+    wv17[ks] = sm[SM_WV + t * (kD + 2) + kD + 1];
+    wc0[ks] = sm[SM_WC + L * kT + 4 * q1 + ks];                 // Wc rows 0..15
+    wc1[ks] = sm[SM_WC + (16 + L7) * kT + 4 * q1 + ks];        // Wc rows 16..23
+  }
+  asm volatile("" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(bw[0]), "+v"(bw[1]),
+               "+v"(bw[2]), "+v"(bw[3]));
+  asm volatile("" : "+v"(wc0[0]), "+v"(wc0[1]), "+v"(wc0[2]), "+v"(wc0[3]), "+v"(wc1[0]),
+               "+v"(wc1[1]), "+v"(wc1[2]), "+v"(wc1[3]));
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    av[ks] = L < kT ? av[ks] : 0.f;
+    bw[ks] = L < kT ? bw[ks] : 0.f;
+    wc0[ks] = q < 2 ? wc0[ks] : 0.f;
+    wc1[ks] = (q < 2 && L < kL2 - 16) ? wc1[ks] : 0.f;
+  }
+  f32x4 k1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) k1 = mfma4(av[ks], bw[ks], k1);   // K1[4q + i][L]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v = k1[i];
+    v = L == 8 ? wv16[i] : L == 9 ? wv17[i] : L == 10 ? 1.f : L == 11 ? 0.f : v;
+    k1[i] = (q < 2 && L < kKA) ? v : 0.f;
+  }
+  f32x4 ka = {0.f, 0.f, 0.f, 0.f}, kb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    ka = mfma4(wc0[ks], k1[ks], ka);                               // K2[4q + i][L]
+    kb = mfma4(wc1[ks], k1[ks], kb);                               // K2[16 + 4q + i][L]
+  }
+  if (L < kKA) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 4 * q + i;
+      if (q < 2) c.sm[SM_K1 + t * kKA + L] = k1[i];
+      c.sm[SM_K2 + t * kKA + L] = ka[i];
+      if (16 + t < kL2) c.sm[SM_K2 + (16 + t) * kKA + L] = kb[i];
+    }
+  }
+}
+
+// Chunk staging shared by both roles (every wave takes part).  The chunk's
+// position window is in flight by LDS-DMA.  Wait, barrier; the producer
+// waves compute the embedding-row tiles (scene_vtile) and, at the first
+// chunk, K1 / K2 (scene_kmats) while `rec_init` runs on the recurrence
+// waves (softmax(h) numerators); barrier.
+template <int NT, int NP, int VMC, typename RecInit>
+__device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout& lay,
+                                            const SceneCtx& c, int fb, int cnt, bool hl,
+                                            RecInit rec_init) {
+  const int wcc = (cnt - 1) * a.d.stride + kT;
+  // VMC = vector-memory ops this wave issued after the LDS-DMA that may stay
+  // in flight (the recurrence's h loads at the first chunk, when hl)
+  if (VMC > 0 && fb == 0 && hl) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                                              // B1: window + weights landed
+  if (c.wv >= kRecW) {
+    const int ntile = (wcc + 3 + 15) / 16;
+    const int ntask = ntile + (fb == 0 ? 1 : 0);
+    for (int task = c.wv - kRecW; task < ntask; task += NP) {
+      if (task < ntile) scene_vtile(a, lay, c, 16 * task, wcc);
+      else scene_kmats(c);
+    }
+  } else {
+    rec_init();
+  }
+  __syncthreads();                                              // B2: V, VG, K1, K2
+}
+
+// Role 1: the recurrence (waves 0..3).  Without h_in (gradient only) the
+// waves only take part in the chunk barriers.
+template <int TPW, int NP>
+__device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneLayout& lay,
+                                                 const SceneCtx& c) {
+  constexpr int NT = 64 * (kRecW + NP);
+  constexpr int kRB = 16 * kRecW;
+  const int H = a.d.H;
+  const bool live = a.h_in != nullptr;
+  Recur<TPW, kRecW> rc;
+  asm volatile("" ::: "memory");   // h loads after the prologue's LDS-DMA (counted vmcnt)
+  if (live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
+  asm volatile("" ::: "memory");
+  int* seq = reinterpret_cast<int*>(c.sRed + 2 * kRB);   // 2 partial buffers, seq words, row max
+  for (int fb = 0; fb < c.nf; fb += lay.fc) {
+    const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
+    if (fb > 0) scene_pos_dma<NT>(a, lay, c, fb, cnt);
+    scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, live, [&] {
+      // softmax(h) numerators (first chunk): row max exchange (seq 1), then
+      // e and its row partials into buffer 0 (seq 2), no workgroup barrier
+      if (fb == 0 && live) {
+        rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
+        asm volatile("" ::: "memory");
+        if (c.lane == 0) lds_store_flag(seq + c.wv, 1);
+        poll_seq(seq + (c.L & 3), 1);
+        rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
+        asm volatile("" ::: "memory");
+        if (c.lane == 0) lds_store_flag(seq + c.wv, 2);
+      }
+    });
+    if (live) {
+      __builtin_amdgcn_s_setprio(2);
+      const float* as_lane = c.sRing + c.L * kD + 4 * c.q;   // this lane's As row quad, ring slot 0
+      // one frame; (b, flq): this frame's prefetched As quad and flag, (bn,
+      // fln): where the next frame's prefetch goes.  Unrolled by two with the
+      // pairs swapped so that a prefetch never needs a register copy (a copy
+      // at the loop edge waits for every outstanding LDS op, the publish too).
+      auto frame = [&](int fl, float4& b, int& flq, float4& bn, int& fln) {
+        const int g = fb + fl;                 // global frame index
+        float4 z;
+        poll_red(seq + (c.L & 3), g + 2, c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, z);
+        if (__builtin_amdgcn_readfirstlane(flq) != g + 1)
+          wait_as(c.sFlag + fl, g + 1, as_lane + fl * kD * kD, b);
+        const int fn = fl + 1 < cnt ? fl + 1 : fl;   // next frame's ring slot (itself at the end)
+        rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,
+                    as_lane + fn * kD * kD, fln, bn);
+      };
+      float4 b0, b1;
+      int f0 = read_as(c.sFlag, as_lane, b0), f1 = 0;
+      for (int fl = 0; fl < cnt; fl += 2) {
+        frame(fl, b0, f0, b1, f1);
+        if (fl + 1 < cnt) frame(fl + 1, b1, f1, b0, f0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
+  }
+  if (!live) return;
+  // epilogue straight off the last frame: wait for every wave's last
+  // partials (its sequence word), h = adj * h', store; no workgroup barrier
+  // (the producers finish the metrics on their own, scene_producer)
+  if (c.nf > 0) poll_seq_all(seq, c.nf + 2);
+  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L,
+           c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);
+}
+
+// One 16-pedestrian tile of one frame: Y^T = Wo^T @ M^T (M = this frame's
+// [24][8] from the M ring; models/g2k_lstm_mcr.py:122-124), pred stores
+// (active columns only, in groups of four), the a9 error terms (train.py:
+// 640-656; four lanes per pedestrian, three prediction steps each).
+// GRAD: dY = (Y - target) on active, masked pedestrians replaces Y in the
+// tile scratch, its squares go to lsum, and the tile's products are formed:
+//   dM   += dY @ Wo^T   (added into the frame's dM [24][8] in LDS)
+//   dWoT  = dY^T @ M    (lane (L, q) reg v: dWo[t = L][n0 + 4q + v])
+template <bool GRAD>
+__device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, float* pr,
+                                          const float2 (&tg)[3], const uint8_t* pm, int Nmax,
+                                          int nact, int t, int L, int q, int lane, float acc[5],
+                                          float& lsum, float* dM, f32x4& dWoT) {
+  const int pp = lane >> 2, u = lane & 3;
+  const int n0 = 16 * t;
+  const int ne = n0 + pp;
+  const bool has_t = ne < nact && (pm ? pm[ne] != 0 : true);
+  f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int n = n0 + L, k = 4 * ks + q;
+    const float wo = n < nact ? sWo[k * Nmax + n] : 0.f;
+    const float bx = L < kL ? M[L * kT + k] : 0.f;
+    const float by = L < kL ? M[(kL + L) * kT + k] : 0.f;
+    y0 = mfma4(wo, bx, y0);   // Y[L][n0 + 4q + i]
+    y1 = mfma4(wo, by, y1);   // Y[12 + L][n0 + 4q + i]
+  }
+  if (L < kL) {
+    const int nb = n0 + 4 * q;
+    if (pr && nb < nact) {    // padded columns (n >= n_active) are left untouched
+      if (nb + 3 < Nmax && ((Nmax & 3) == 0)) {
+        *reinterpret_cast<float4*>(pr + L * Nmax + nb) = make_float4(y0[0], y0[1], y0[2], y0[3]);
+        *reinterpret_cast<float4*>(pr + (kL + L) * Nmax + nb) = make_float4(y1[0], y1[1], y1[2], y1[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (nb + i < Nmax) { pr[L * Nmax + nb + i] = y0[i]; pr[(kL + L) * Nmax + nb + i] = y1[i]; }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float2*>(ys + (4 * q + i) * kL2 + 2 * L) = make_float2(y0[i], y1[i]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f, fx = 0.f, fy = 0.f;
+  float2* yp = reinterpret_cast<float2*>(ys + pp * kL2) + 3 * u;
+  float2 dyv[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float2 yv = yp[k];
+    const float dx = yv.x - tg[k].x, dy = yv.y - tg[k].y;
+    ea = fmaf(dx, dx, ea);
+    eb = fmaf(dx, dy, eb);
+    ec = fmaf(dy, dy, ec);
+    el2 += __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
+    fx = dx; fy = dy;
+    dyv[k] = make_float2(has_t ? dx : 0.f, has_t ? dy : 0.f);
+  }
+  if (GRAD) {
+    lsum += has_t ? ea + ec : 0.f;           // this lane's three steps
+#pragma unroll
+    for (int k = 0; k < 3; ++k) yp[k] = dyv[k];   // dY over Y, in place (own entries only)
+  }
+  __builtin_amdgcn_wave_barrier();
+  ea += dpp<0xB1>(ea); ea += dpp<0x4E>(ea);
+  eb += dpp<0xB1>(eb); eb += dpp<0x4E>(eb);
+  ec += dpp<0xB1>(ec); ec += dpp<0x4E>(ec);
+  el2 += dpp<0xB1>(el2); el2 += dpp<0x4E>(el2);
+  fx = dpp<0xFF>(fx);   // quad_perm [3,3,3,3]: the fde vector lives in quarter 3
+  fy = dpp<0xFF>(fy);
+  if (has_t && u == 0) {
+    const float hm = 0.5f * (ea - ec);
+    const float lam = 0.5f * (ea + ec) + __builtin_amdgcn_sqrtf(fmaf(hm, hm, eb * eb));
+    const float fsq = fmaf(fx, fx, fy * fy);
+    acc[0] += __builtin_amdgcn_sqrtf(fmaxf(lam, 0.f)) * (1.0f / 12.0f);
+    acc[1] += 1.0f;
+    acc[2] += fsq;
+    acc[3] += el2 * (1.0f / 12.0f);
+    acc[4] += __builtin_amdgcn_sqrtf(fsq);
+  }
+  if (GRAD) {
+    // the dY entries of other lanes: LDS in order within the wave, so only
+    // the compiler has to be kept from moving the reads above the writes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // dM += dY @ Wo^T: A[r = L][k] = dY[r][n0 + k], B[k][t = L] = Wo[t][n0 + k], k = 4q + ks
+    {
+      float ax[4], ay[4], bw[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k = 4 * q + ks;
+        const float2 d = *reinterpret_cast<const float2*>(ys + k * kL2 + 2 * (L < kL ? L : 0));
+        ax[ks] = L < kL ? d.x : 0.f;
+        ay[ks] = L < kL ? d.y : 0.f;
+        const int n = n0 + k;
+        bw[ks] = (L < kT && n < nact) ? sWo[(L & 7) * Nmax + (n < Nmax ? n : 0)] : 0.f;
+      }
+      f32x4 mx = {0.f, 0.f, 0.f, 0.f}, my = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        mx = mfma4(ax[ks], bw[ks], mx);
+        my = mfma4(ay[ks], bw[ks], my);
+      }
+      // into the frame's dM [24][8] (this wave's scratch), tile after tile
+      if (L < kT && q < 3) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          dM[(4 * q + v) * kT + L] += mx[v];
+          dM[(kL + 4 * q + v) * kT + L] += my[v];
+        }
+      }
+    }
+    // dWo^T = dY^T @ M: A[n = L][r] = dY[r][n0 + L], B[r][t = L] = M[r][t], r = 4 ks + q
+    {
+      float ar[6], br[6];
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        const int r = 4 * ks + q;
+        const int col = r < kL ? 2 * r : 2 * (r - kL) + 1;
+        ar[ks] = ys[L * kL2 + col];
+        br[ks] = L < kT ? M[r * kT + (L & 7)] : 0.f;
+      }
+      f32x4 w = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) w = mfma4(ar[ks], br[ks], w);
+      dWoT = w;
+    }
+  }
+}
+
+// LDS hand-off between the lanes of ONE wave: DS instructions of a wave
+// complete in issue order, so only compiler reordering has to be fenced
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wait (one LDS word, wave-uniform) until *w == want.
+__device__ __forceinline__ void poll_word(const int* w, int want) { poll_flag(w, want); }
+
+// GRAD, after the last tile of frame f (chunk slot fl): the frame's
+// weight-side terms on the VALU of this wave (one lane per output entry),
+// then their addition into the scene's accumulators in frame order.
+//   dcost[u][t] = sum_r Wc[r][u] dM[r][t]          (M = Wc @ cost, :119)
+//   dE[t][d]    = lambda sum_u dcost[t][u] G[d][u] (cost = E @ g, :112-113)
+//   dWc_f[r][u] = sum_t dM[r][t] cost[u][t]
+//   dK1_f[t][j] = sum_d dE[t][d] Uaug[j][d]        (E = K1 @ Uaug, j < 10)
+//   dUaug_f[j][d] = sum_t K1[t][j] dE[t][d]        (j < 8: window rows, 8-9: Ve, 10: bv)
+__device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout& lay,
+                                           const SceneCtx& c, int fb, int fl) {
+  float* gf = c.sGFrame + (c.wv - kRecW) * kGFrame;
+  float* dM = gf + kGT_DM;
+  float* dC = gf + kGT_DC;
+  float* dE = gf + kGT_DE;
+  float* tm = gf + kGT_TERMS;
+  const int L = c.L, q = c.q, lane = c.lane;
+  const float* sm = c.sm;
+  (void)L; (void)q;
+  wave_lds_sync();                                        // the frame's dM, all tiles added
+  {
+    const int u = lane >> 3, tt = lane & 7;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < kL2; r += 2) {
+      s0 = fmaf(sm[SM_WC + r * kT + u], dM[r * kT + tt], s0);
+      s1 = fmaf(sm[SM_WC + (r + 1) * kT + u], dM[(r + 1) * kT + tt], s1);
+    }
+    dC[lane] = s0 + s1;
+  }
+  wave_lds_sync();
+#pragma unroll 1
+  for (int o = lane; o < kT * kD; o += 64) {
+    const int t = o >> 4, d = o & 15;
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < kT; ++u) s = fmaf(dC[t * kT + u], sm[SM_G + d * kT + u], s);
+    dE[o] = a.lambda * s;
+  }
+  wave_lds_sync();
+  const float* cost = c.sCost + fl * kT * kT;
+  const int wrow0 = fl * a.d.stride;
+#pragma unroll 1
+  for (int o = lane; o < kL2 * kT; o += 64) {             // dWc_f
+    const int r = o >> 3, u = o & 7;
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < kT; ++t) s = fmaf(dM[r * kT + t], cost[u * kT + t], s);
+    tm[o] = s;
+  }
+  for (int o = lane; o < kT * 10; o += 64) {              // dK1_f
+    const int t = o / 10, j = o - t * 10;
+    const float* ur = c.sV + (j < kT ? wrow0 + j : lay.wcmax + (j - kT)) * kD;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int d = 0; d < kD; d += 2) {
+      s0 = fmaf(dE[t * kD + d], ur[d], s0);
+      s1 = fmaf(dE[t * kD + d + 1], ur[d + 1], s1);
+    }
+    tm[kL2 * kT + o] = s0 + s1;
+  }
+#pragma unroll 1
+  for (int o = lane; o < 11 * kD; o += 64) {              // dUaug_f
+    const int j = o >> 4, d = o & 15;
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < kT; ++t) s = fmaf(sm[SM_K1 + t * kKA + j], dE[t * kD + d], s);
+    tm[kL2 * kT + kT * 10 + o] = s;
+  }
+  wave_lds_sync();
+  for (int o = lane; o < kL2 * kT; o += 64) dM[o] = 0.f;  // for this wave's next frame
+  const int f = fb + fl;
+  poll_word(c.sGseq, f);                                  // frames < f added
+  float* ga = c.sGAcc;
+#pragma unroll 1
+  for (int o = lane; o < kGTerms; o += 64) {
+    const float v = tm[o];
+    if (o < kL2 * kT) {
+      ga[kGA_WC + o] += v;
+    } else if (o < kL2 * kT + kT * 10) {
+      ga[kGA_K1 + o - kL2 * kT] += v;
+    } else {
+      const int p = o - kL2 * kT - kT * 10, j = p >> 4, d = p & 15;
+      if (j < kT) c.sGdV[(f * a.d.stride + j) * kD + d] += v;
+      else if (j < kT + 2) ga[kGA_VE + (j - kT) * kD + d] += v;
+      else ga[kGA_BV + d] += v;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) lds_store_flag(c.sGseq, f + 1);
+}
+
+// Role 2: the producers (waves 4..4+NP-1).
+template <int NP, bool GRAD>
+__device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLayout& lay,
+                                               const SceneCtx& c) {
+  const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
+  const int pw = c.wv - kRecW, L = c.L, q = c.q, lane = c.lane, s = c.s, ntact = c.ntact;
+  const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
+  // tile items of a chunk.  Forward: item j -> frame j / ntact, tile
+  // j % ntact; this producer takes items pw, pw + NP, ...  GRAD: this
+  // producer owns whole frames pw, pw + NP, ... (its k-th item is tile
+  // k % ntact of its (k / ntact)-th frame)
+  const int pp = lane >> 2, u = lane & 3;
+  auto item_ft = [&](int k, int& fl, int& t) {
+    if (GRAD) {
+      fl = pw + (k / ntact) * NP;
+      t = k - (k / ntact) * ntact;
+    } else {
+      const int j = pw + k * NP;
+      fl = j / ntact;
+      t = j - fl * ntact;
+    }
+  };
+  float2 tgA[3] = {}, tgB[3] = {};
+  auto load_item = [&](int fb, int nitems, int k, float2 (&tg)[3]) {
+    if (k >= nitems) return;
+    int fl, t;
+    item_ft(k, fl, t);
+    const int ne = 16 * t + pp;
+    const int nc = ne < Nmax ? ne : 0;
+    const float2* tp = reinterpret_cast<const float2*>(
+        a.targets + (((size_t)s * F + fb + fl) * Nmax + nc) * kL2) + 3 * u;
+    tg[0] = tp[0]; tg[1] = tp[1]; tg[2] = tp[2];
+  };
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float lsum = 0.f;
+  if (GRAD) {                                          // this wave's dM starts at zero
+    float* dM0 = c.sGFrame + pw * kGFrame + kGT_DM;
+    for (int o = lane; o < kL2 * kT; o += 64) dM0[o] = 0.f;
+  }
+  for (int fb = 0; fb < c.nf; fb += lay.fc) {
+    const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
+    if (fb > 0) scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
+    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});
+    int nitems;
+    if (GRAD) {
+      const int nfr = cnt > pw ? (cnt - pw + NP - 1) / NP : 0;
+      nitems = nfr * ntact;
+    } else {
+      nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;
+    }
+    load_item(fb, nitems, 0, tgA);    // first tiles' targets: in flight during the heads
+    load_item(fb, nitems, 1, tgB);
+    // Rm = Wr @ Rel, Rel = Ve * Ve (train.py:194-195, g2k_lstm_mcr.py:106):
+    // rows t = 4q + i of column L, zero for t >= 8
+    float rm[4];
+    {
+      const float ve0 = c.sV[lay.wcmax * kD + L], ve1 = c.sV[(lay.wcmax + 1) * kD + L];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = 4 * q + i;
+        rm[i] = q < 2 ? fmaf(c.sm[SM_WR + 2 * t], ve0 * ve0, c.sm[SM_WR + 2 * t + 1] * (ve1 * ve1)) : 0.f;
+      }
+    }
+    // phase 1 — the critical path: frame heads in frame order, As and M into
+    // the rings, then the frame's flags; the first heads the recurrence will
+    // wait for get the issue priority
+    for (int fl = pw; fl < cnt; fl += NP) {
+      const int f = fb + fl;
+      if (fl < kRecW) __builtin_amdgcn_s_setprio(1);
+      const FrameHeadOut hd =
+          frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
+                     a.A_out ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
+                     a.cost_out ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr,
+                     GRAD ? c.sCost + fl * kT * kT : nullptr, L, q);
+      if (L < kL && q < 2) {
+        float* m = c.sMring + fl * kL2 * kT;
+        *reinterpret_cast<float4*>(m + L * kT + 4 * q) = make_float4(hd.mT0[0], hd.mT0[1], hd.mT0[2], hd.mT0[3]);
+        *reinterpret_cast<float4*>(m + (kL + L) * kT + 4 * q) = make_float4(hd.mT1[0], hd.mT1[1], hd.mT1[2], hd.mT1[3]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        lds_store_flag(c.sMflag + fl, f + 1);
+        lds_store_flag(c.sFlag + fl, f + 1);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // phase 2 — predictions and errors (GRAD: and the gradient)
+    float* ys = c.sY + pw * kD * kL2;
+    float* dMs = GRAD ? c.sGFrame + pw * kGFrame + kGT_DM : nullptr;
+    auto item = [&](int k, const float2 (&tg)[3]) {
+      int fl, t;
+      item_ft(k, fl, t);
+      const int f = fb + fl;
+      poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)
+      float* pr = a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : nullptr;
+      f32x4 dWoT;
+      pred_tile<GRAD>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, pm, Nmax, c.nact, t, L, q, lane,
+                      acc, lsum, dMs, dWoT);
+      if (GRAD) {
+        // dWo^T[n0 + 4q + v][t = L]: one copy per producer, or one copy
+        // added to in frame order (tile sequence word) when that is too big
+        const int nb = 16 * t + 4 * q;
+        float* dst = c.sGdWo + (lay.dwo_seq ? 0 : pw * Nmax * kT);
+        if (lay.dwo_seq) poll_word(c.sGseq + 2 + t, f);
+        if (L < kT) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (nb + v < Nmax) dst[(nb + v) * kT + L] += dWoT[v];
+        }
+        if (lay.dwo_seq) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (lane == 0) lds_store_flag(c.sGseq + 2 + t, f + 1);
+        }
+      }
+    };
+    if (GRAD) {
+      // frame by frame: tiles in pairs (even tiles in buffer A, odd in B),
+      // each buffer prefetching its next tile of the same parity — in this
+      // frame, else tile 0 (A) / 1 (B) of this producer's next frame — and
+      // the frame's weight-side terms after its last tile (one call site)
+      const int nfr = nitems / (ntact > 0 ? ntact : 1);
+      auto prefetch = [&](int fi, int t, float2 (&tg)[3]) {
+        const int tn = t + 2 < ntact ? t + 2 : (t & 1);
+        const int fn = t + 2 < ntact ? fi : fi + 1;
+        if (fn < nfr && tn < ntact) load_item(fb, nitems, fn * ntact + tn, tg);
+      };
+      for (int fi = 0; fi < nfr; ++fi) {
+        for (int t = 0; t < ntact; t += 2) {
+          item(fi * ntact + t, tgA);
+          prefetch(fi, t, tgA);
+          if (t + 1 < ntact) {
+            item(fi * ntact + t + 1, tgB);
+            prefetch(fi, t + 1, tgB);
+          }
+        }
+        frame_grad(a, lay, c, fb, pw + fi * NP);
+      }
+    } else {
+      for (int k = 0; k < nitems; k += 2) {
+        item(k, tgA);
+        load_item(fb, nitems, k + 2, tgA);
+        if (k + 1 < nitems) {
+          item(k + 1, tgB);
+          load_item(fb, nitems, k + 3, tgB);
+        }
+      }
+    }
+    if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
+  }
+  // metrics (and the loss): each producer publishes its partial sums, then
+  // takes a ticket (LDS atomic); the wave drawing the last ticket sums the
+  // NP rows in producer order (deterministic) and writes the scene's row
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const float v = wave_sum(acc[k]);
+    if (lane == 0) c.sMet[pw * 8 + k] = v;
+  }
+  if (GRAD) {
+    const float v = wave_sum(lsum);
+    if (lane == 0) c.sMet[pw * 8 + 5] = v;
+  }
+  int ticket = 0;
+  if (lane == 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // partials before the ticket
+    ticket = atomicAdd(c.sTicket, 1);
+  }
+  ticket = __builtin_amdgcn_readfirstlane(ticket);
+  if (ticket == NP - 1 && lane < 8 && a.metrics) {
+    float v = 0.f;
+    if (lane < 5) {
+      if (c.nf > 0)
+        for (int p = 0; p < NP; ++p) v += c.sMet[p * 8 + lane];
+    } else if (lane == 5) {
+      v = (float)c.nf;
+    }
+    a.metrics[(size_t)s * 8 + lane] = v;
+  }
+  if (!GRAD) return;
+  // GRAD: every producer has added its frames once the ticket count is NP;
+  // then the scene's gradient row [P + 2] (g2k_weights order) is formed by
+  // all producers together
+  poll_word(c.sTicket, NP);
+  const int P = 24 * Nmax + 496;
+  float* row = a.grad_rows + (size_t)s * (P + 2);
+  const float* ga = c.sGAcc;
+  const float* sm = c.sm;
+  const int o_wii = Nmax * kD, o_wv = o_wii + kD * kT, o_bv = o_wv + kT * (kD + 2),
+            o_wr = o_bv + kD, o_wc = o_wr + kT * 2, o_wo = o_wc + kL2 * kT;
+  // dWi[n][d] = sum_w N[w][n] dV[w][d] + vislet[0][n] dVe[0][d] + vislet[1][n] dVe[1][d]
+  // (train.py:76-85 norms of the whole window, re-read from the position rows)
+  // by MFMA per 16-pedestrian tile: A[n = L][w] = N[w][n0 + L], B[w][d = L] = dV[w][d]
+  const int ntile_all = (Nmax + 15) >> 4;
+  #pragma unroll 1
+  for (int t = pw; t < ntile_all; t += NP) {
+    const int n0 = 16 * t, n = n0 + L;
+    f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
+    if (n0 < c.nact) {
+      const float* prow = a.pos + (size_t)c.s * a.d.W * Nmax * 2;
+      const int nks = (lay.wtot + 3) / 4;
+      #pragma unroll 1
+      for (int ks = 0; ks < nks; ++ks) {
+        const int w = 4 * ks + q;
+        float av = 0.f, bv = 0.f;
+        if (w < lay.wtot) {
+          if (n < c.nact) {
+            const float2 p = *reinterpret_cast<const float2*>(prow + ((size_t)w * Nmax + n) * 2);
+            av = __builtin_amdgcn_sqrtf(fmaf(p.x, p.x, p.y * p.y));
+          }
+          bv = c.sGdV[w * kD + L];
+        }
+        acc4 = mfma4(av, bv, acc4);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int nn = n0 + 4 * q + v;
+      if (nn < Nmax) {
+        float x = acc4[v];
+        if (nn < c.nact)
+          x += fmaf(c.sVis[nn], ga[kGA_VE + L], c.sVis[Nmax + nn] * ga[kGA_VE + kD + L]);
+        row[nn * kD + L] = x;
+      }
+    }
+  }
+  // the small blocks and dWo, entry by entry over all producer lanes
+  const int ptid = pw * 64 + lane;
+  #pragma unroll 1
+  for (int p = o_wii + ptid; p < P + 2; p += NP * 64) {
+    float x = 0.f;
+    if (p < o_wv) {                                   // dWii[c][u] = sum_t Wv[t][c] AU[t][u]
+      const int q2 = p - o_wii, cc = q2 >> 3, uu = q2 & 7;
+#pragma unroll
+      for (int t = 0; t < kT; ++t) x = fmaf(sm[SM_WV + t * (kD + 2) + cc], ga[kGA_K1 + t * 10 + uu], x);
+    } else if (p < o_bv) {                            // dWv
+      const int q2 = p - o_wv, t = q2 / (kD + 2), cc = q2 - t * (kD + 2);
+      if (cc < kD) {
+#pragma unroll
+        for (int uu = 0; uu < kT; ++uu) x = fmaf(ga[kGA_K1 + t * 10 + uu], sm[SM_WII + cc * kT + uu], x);
+      } else {
+        x = ga[kGA_K1 + t * 10 + kT + (cc - kD)];
+      }
+    } else if (p < o_wr) {
+      x = ga[kGA_BV + p - o_bv];
+    } else if (p < o_wc) {
+      x = 0.f;                                        // Wr does not reach the predictions
+    } else if (p < o_wo) {
+      x = ga[kGA_WC + p - o_wc];
+    } else if (p < P) {                               // dWo[t][n]
+      const int q2 = p - o_wo, t = q2 / Nmax, nn = q2 - t * Nmax;
+      if (lay.dwo_seq) {
+        x = c.sGdWo[nn * kT + t];
+      } else {
+        for (int pr = 0; pr < NP; ++pr) x += c.sGdWo[(pr * Nmax + nn) * kT + t];
+      }
+    } else if (p == P) {                              // loss = 1/2 sum dY^2, producer order
+      for (int pr = 0; pr < NP; ++pr) x += c.sMet[pr * 8 + 5];
+      x *= 0.5f;
+    } else {                                          // count of (frame, pedestrian) pairs
+      for (int pr = 0; pr < NP; ++pr) x += c.sMet[pr * 8 + 1];
+    }
+    row[p] = x;
+  }
+}
+
+template <int TPW, int NP, bool GRAD>
+__global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a, SceneLayout lay) {
+  constexpr int NT = 64 * (kRecW + NP);
+  constexpr int kRB = 16 * kRecW;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  SceneCtx c;
+  c.s = blockIdx.x;
+  c.tid = threadIdx.x; c.lane = c.tid & 63; c.wv = wave_id(); c.L = c.lane & 15; c.q = c.lane >> 4;
+  const int Nmax = a.d.Nmax, F = a.d.F;
+  c.ntiles = (Nmax + 15) >> 4;
+  c.sWi = smem + lay.o_wi; c.sWo = smem + lay.o_wo; c.sVis = smem + lay.o_vis; c.sV = smem + lay.o_v;
+  c.sm = smem + lay.o_small; c.sMet = smem + lay.o_met; c.sRing = smem + lay.o_ring;
+  c.sMring = smem + lay.o_mring; c.sRed = smem + lay.o_red; c.sPos = smem + lay.o_pos;
+  c.sVG = smem + lay.o_vg;
+  c.sFlag = reinterpret_cast<int*>(smem + lay.o_flag);
+  c.sMflag = reinterpret_cast<int*>(smem + lay.o_mflag);
+  c.sY = smem + lay.o_y;
+  c.sTicket = reinterpret_cast<int*>(c.sRed + 2 * kRB) + kRecW;
+  c.sCost = smem + lay.o_cost; c.sGFrame = smem + lay.o_gframe; c.sGAcc = smem + lay.o_gacc;
+  c.sGdV = smem + lay.o_gdv; c.sGdWo = smem + lay.o_gdwo;
+  c.sGseq = reinterpret_cast<int*>(smem + lay.o_gseq);
+  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket
+  if (GRAD) {                                          // accumulators and their sequence words
+    for (int i = c.tid; i < lay.o_gseq + rup4(2 + c.ntiles) - lay.o_gacc; i += NT) smem[lay.o_gacc + i] = 0.f;
+  }
+  if (F > 0) {
+    // issued before n_active / n_frames arrive: the first chunk's window for
+    // min(F, fc) frames (a scene with fewer frames reads rows it ignores)
+    const int wv = c.wv, lane = c.lane;
+    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
+    // the small segments: one wave each (one pointer per wave keeps the
+    // kernel-argument loads off a serial s_load / s_waitcnt chain)
+    for (int seg = wv; seg < 10; seg += NT / 64) {
+      const float* src;
+      float* dst;
+      int n;
+      switch (seg) {
+        case 0: src = a.w.Wi; dst = c.sWi; n = Nmax * kD; break;
+        case 1: src = a.w.Wo; dst = c.sWo; n = kT * Nmax; break;
+        case 2: src = a.w.Wii; dst = c.sm + SM_WII; n = kD * kT; break;
+        case 3: src = a.G + (size_t)c.s * kD * kT; dst = c.sm + SM_G; n = kD * kT; break;
+        case 4: src = a.w.Wv; dst = c.sm + SM_WV; n = kT * (kD + 2); break;
+        case 5: src = a.w.bv; dst = c.sm + SM_BV; n = kD; break;
+        case 6: src = a.w.Wr; dst = c.sm + SM_WR; n = kT * 2; break;
+        case 7: src = a.w.Wc; dst = c.sm + SM_WC; n = kL2 * kT; break;
+        case 8: src = a.vislet + (size_t)c.s * 2 * Nmax; dst = c.sVis; n = Nmax; break;
+        default: src = a.vislet + (size_t)c.s * 2 * Nmax + Nmax; dst = c.sVis + Nmax; n = Nmax; break;
+      }
+      for (int i = 0; i < n; i += 64)
+        if (i + lane < n)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i + lane),
+                                           (__attribute__((address_space(3))) void*)(dst + i), 4, 0, 0);
+    }
+    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)
+      c.sFlag[c.tid] = 0;
+      c.sMflag[c.tid] = 0;
+    }
+  }
+  c.nact = clampi(a.n_active[c.s], 0, Nmax);
+  c.nf = a.n_frames ? clampi(a.n_frames[c.s], 0, F) : F;
+  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians
+  if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
+  if (c.wv < kRecW)
+    scene_recurrence<TPW, NP>(a, lay, c);
+  else
+    scene_producer<NP, GRAD>(a, lay, c);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
+}
+
+// Fused scene kernel geometry: producer waves (NP).  Measured (round 1,
+// 400 steps): eth_hotel_synth (H 128, Nmax 32) NP 8 19.9 us vs NP 12 20.2,
+// NP 6 22.2, NP 4 24.3; H 256 / Nmax 64: NP 12 28.2 vs NP 8 29.6; dense
+// crowd (H 256, Nmax 256): NP 12 53.2 vs NP 8 60.5; k-fold (H 128, Nmax 64):
+// NP 12 23.6 vs NP 8 25.4.  So 12 producers (16 waves, 4 per SIMD) once
+// H >= 256 or Nmax >= 64, else 8; H = 512 needs > 128 VGPRs per wave: 4.
+// Train mode keeps 8 (its producers need more than the 128 VGPRs per wave
+// that 16 waves leave).
+int scene_producers(int H, int Nmax, bool grad) {
+  if (H >= 512) return 4;
+  if (grad) return 8;
+  return (H >= 256 || Nmax >= 64) ? 12 : 8;
+}
+
+template <int TPW, int NP, bool GRAD>
+void launch_k(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
+  hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD>), dim3(a.d.S), dim3(64 * (kRecW + NP)),
+                     (size_t)l.total * 4, st, a, l);
+}
+
+template <bool GRAD>
+int launch_np(const StepArgs& a, const SceneLayout& l, int NP, int tpw, hipStream_t st) {
+  if (NP == 4 && tpw == 8) { launch_k<8, 4, GRAD>(a, l, st); return G2K_OK; }
+  if (NP == 8) {
+    switch (tpw) {
+      case 1: launch_k<1, 8, GRAD>(a, l, st); return G2K_OK;
+      case 2: launch_k<2, 8, GRAD>(a, l, st); return G2K_OK;
+      case 4: launch_k<4, 8, GRAD>(a, l, st); return G2K_OK;
+      default: break;
+    }
+  } else if (NP == 12 && !GRAD) {
+    switch (tpw) {
+      case 1: launch_k<1, 12, false>(a, l, st); return G2K_OK;
+      case 2: launch_k<2, 12, false>(a, l, st); return G2K_OK;
+      case 4: launch_k<4, 12, false>(a, l, st); return G2K_OK;
+      default: break;
+    }
+  }
+  return set_err(G2K_EUNSUPPORTED, "scene kernel not built for H=%d (NP=%d)", a.d.H, NP);
+}
+
+}  // namespace
+
+int64_t scene_lds_bytes(const g2k_dims* d, bool grad) {
+  const int H = grad && d->H < 64 ? 64 : d->H;
+  return (int64_t)scene_layout(d, scene_producers(H, d->Nmax, grad), grad).total * 4;
+}
+
+int scene_step_launch(const StepArgs& a, hipStream_t st) {
+  const bool grad = a.grad_rows != nullptr;
+  // gradient only (no h_in): the recurrence waves idle, the smallest build
+  const int H = a.h_in ? a.d.H : 64;
+  const int NP = scene_producers(H, a.d.Nmax, grad);
+  const SceneLayout l = scene_layout(&a.d, NP, grad);
+  if ((int64_t)l.total * 4 > 160 * 1024)
+    return set_err(G2K_ELDS, "Nmax=%d, stride=%d needs %lld bytes of LDS", a.d.Nmax, a.d.stride,
+                   (long long)l.total * 4);
+  const int tpw = H / 64;
+  const int rc = grad ? launch_np<true>(a, l, NP, tpw, st) : launch_np<false>(a, l, NP, tpw, st);
+  if (rc) return rc;
+  return check_launch(grad ? "g2k_scene_kernel (train)" : "g2k_scene_kernel");
+}
+
+}  // namespace g2k

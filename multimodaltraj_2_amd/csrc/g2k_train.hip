@@ -1,0 +1,123 @@
+// g2k_train.hip — train mode after the fused step (SURVEY.md §8(d) "--mode
+// train", §8(e) gradient all-reduce): the per-scene gradient rows written
+// by g2k_scene_kernel<..., GRAD> summed over scenes in a fixed order, and the
+// optimizer update.  The reference has no loss or optimizer (SURVEY.md
+// finding 5); the update follows the flags it parses (argParser.py:38-47).
+#include "g2k_common.h"
+
+namespace g2k {
+namespace {
+
+// grad[p] = sum_s rows[s][p]: workgroup = 64 columns x 4 row slices; slice k
+// sums rows k, k + 4, ... in order, then the four slices in order (the same
+// sum for every launch: deterministic, no atomics)
+__global__ void __launch_bounds__(256) g2k_grad_rows_kernel(const float* __restrict__ rows, int S,
+                                                            int width, float* __restrict__ grad) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int p = blockIdx.x * 64 + c;
+  float a0 = 0.f, a1 = 0.f;
+  if (p < width) {
+    int r = sl;
+    for (; r + 4 < S; r += 8) {           // two rows in flight per step
+      a0 += rows[(size_t)r * width + p];
+      a1 += rows[(size_t)(r + 4) * width + p];
+    }
+    if (r < S) a0 += rows[(size_t)r * width + p];
+  }
+  red[sl][c] = a0 + a1;
+  __syncthreads();
+  if (sl == 0 && p < width) grad[p] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+
+// Optimizer step (argParser.py:38-47: grad_clip, learning_rate, decay_rate):
+// g = grad / count, clipped by global norm (g * clip / max(||g||, clip)),
+// then RMSProp (ms = decay ms + (1 - decay) g^2; p -= lr g / sqrt(ms +
+// 1e-10), TF RMSPropOptimizer without momentum) or SGD (ms NULL).  One
+// workgroup: the norm is a fixed-order block reduction.
+__global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ params,
+                                                          float* __restrict__ ms,
+                                                          const float* __restrict__ grad, int n,
+                                                          float lr, float decay, float clip) {
+  __shared__ float red[16];
+  const int tid = threadIdx.x;
+  // up to kPre entries per thread: parameters and mean squares are loaded
+  // together with the gradient, before the norm's reduction
+  constexpr int kPre = 8;
+  const bool pre = n <= kPre * 1024;
+  float pg[kPre], pp[kPre], pm[kPre];
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int i = tid + j * 1024;
+      pg[j] = i < n ? grad[i] : 0.f;
+      pp[j] = i < n ? params[i] : 0.f;
+      pm[j] = (ms && i < n) ? ms[i] : 0.f;
+    }
+  }
+  const float inv = 1.0f / fmaxf(grad[n + 1], 1.0f);
+  float ss = 0.f;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const float g = pg[j] * inv;
+      ss = fmaf(g, g, ss);
+    }
+  } else {
+    for (int i = tid; i < n; i += 1024) {
+      const float g = grad[i] * inv;
+      ss = fmaf(g, g, ss);
+    }
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) tot += red[w];
+  const float nrm = sqrtf(tot);
+  const float scale = clip > 0.f ? inv * (clip / fmaxf(nrm, clip)) : inv;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int i = tid + j * 1024;
+      if (i >= n) break;
+      const float g = pg[j] * scale;
+      if (ms) {
+        const float m = fmaf(decay, pm[j], (1.f - decay) * g * g);
+        ms[i] = m;
+        params[i] = pp[j] - lr * g / sqrtf(m + 1e-10f);
+      } else {
+        params[i] = fmaf(-lr, g, pp[j]);
+      }
+    }
+    return;
+  }
+  for (int i = tid; i < n; i += 1024) {
+    const float g = grad[i] * scale;
+    if (ms) {
+      const float m = fmaf(decay, ms[i], (1.f - decay) * g * g);
+      ms[i] = m;
+      params[i] -= lr * g / sqrtf(m + 1e-10f);
+    } else {
+      params[i] = fmaf(-lr, g, params[i]);
+    }
+  }
+}
+
+}  // namespace
+
+int grad_rows_launch(const float* rows, int S, int width, float* grad, hipStream_t st) {
+  hipLaunchKernelGGL(g2k_grad_rows_kernel, dim3((width + 63) / 64), dim3(256), 0, st, rows, S, width,
+                     grad);
+  return check_launch("g2k_grad_rows_kernel");
+}
+
+int update_launch(float* params, float* ms, const float* grad, int n, float lr, float decay,
+                  float clip, hipStream_t st) {
+  hipLaunchKernelGGL(g2k_update_kernel, dim3(1), dim3(1024), 0, st, params, ms, grad, n, lr, decay,
+                     clip);
+  return check_launch("g2k_update_kernel");
+}
+
+}  // namespace g2k

@@ -194,8 +194,10 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
         if tuple(ped_mask.shape) != (S, Nmax):
             raise ValueError("ped_mask must be [S, Nmax]")
     if out is None:
+        # the kernel writes pred for frames < n_frames and columns < n_active
+        # only: the rest stays as allocated (zero)
         out = StepOutputs(
-            pred=torch.empty((S, F, 2 * PRED_LEN, Nmax), device=dev, dtype=torch.float32),
+            pred=torch.zeros((S, F, 2 * PRED_LEN, Nmax), device=dev, dtype=torch.float32),
             h=h_out if h_out is not None else torch.empty_like(h),
             metrics=torch.empty((S, 8), device=dev, dtype=torch.float32),
             attn=(torch.empty((S, F, HIDDEN_LEN, HIDDEN_LEN), device=dev, dtype=torch.float32)

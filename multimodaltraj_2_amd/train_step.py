@@ -5,9 +5,10 @@ The reference has no loss, gradient or optimizer for g2k_lstm_mcr (SURVEY.md
 finding 5: its training loop re-initialises weights and fetches fed tensors);
 this mode is the build's, for the north star's "RCCL all-reduce of
 gradients".  loss = 1/2 the squared error of the pred_path_band rows against
-the targets the ADE/FDE use; the gradient comes from g2k_step_grad_f32
-(checked against the float64 oracle ``scene_loss_grad``, itself pinned by
-finite differences; unpinned against the reference, which has none).  One
+the targets the ADE/FDE use; the gradient comes out of the same scene-kernel
+launch as the step's outputs (g2k_train_step_f32; g2k_step_grad_f32 without
+the outputs), checked against the float64 oracle ``scene_loss_grad``, itself
+pinned by finite differences; unpinned against the reference, which has none.  One
 flat [P + 2] buffer (gradient sums, loss, count) is all-reduced per step —
 RCCL over xGMI under the nccl backend, 5.1 KB at Nmax = 32 — then every rank
 applies the same update (RMSProp with global-norm clipping, argParser.py:38-47
@@ -131,38 +132,106 @@ def optimizer_update(flat, grad, *, lr=LEARNING_RATE, decay=DECAY_RATE, grad_cli
     _lib.check("g2k_update_f32", rc)
 
 
-class TrainStep:
-    """One train-mode step over fixed device buffers: the fused reference
-    step (pred, h, ADE/FDE sums), the loss gradient, the all-reduce of the
-    flat gradient across ranks (when a process group is up), the update."""
+class TrainPlan:
+    """A validated launch of ``g2k_train_step_f32`` bound to fixed buffers:
+    the fused step's outputs (pred, h, ADE/FDE sums) and the loss gradient
+    [P + 2] from ONE scene-kernel launch (the producers turn each prediction
+    tile's error into the gradient; nothing is recomputed), the per-scene
+    gradient rows summed in a fixed order, and optionally the update."""
 
-    def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
-                 lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,
-                 n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None):
-        self.flat, self.params = flat_params(params)
-        self.fwd = StepPlan(self.params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
-                            ped_mask=ped_mask, stride=stride, lam=lam, out=out)
-        self.gradplan = GradPlan(self.params, pos, vislet, G, targets, n_active,
-                                 n_frames=n_frames, ped_mask=ped_mask, stride=stride, lam=lam)
-        self.ms = torch.zeros_like(self.flat) if rmsprop else None
-        self.lr, self.decay, self.grad_clip = lr, decay, grad_clip
-        self.group = group
-        self.world = (dist.get_world_size(group)
-                      if dist.is_available() and dist.is_initialized() else 1)
+    def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
+                 ped_mask=None, stride=1, lam=LAMBDA, out=None, grad=None, stream=None):
+        lib = _lib.load()
+        self.fwd = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
+                            ped_mask=ped_mask, stride=stride, lam=lam, out=out, stream=stream)
+        dev = pos.device
+        S, W, Nmax, _ = pos.shape
+        F, H = int(targets.shape[1]), int(h.shape[2])
+        d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride)
+        self.P = int(lib.g2k_grad_size(ctypes.byref(d)))
+        nws = int(lib.g2k_train_workspace_bytes(ctypes.byref(d)))
+        if self.P < 0 or nws < 0:
+            _lib.check("g2k_train_workspace_bytes", -1)
+        self.grad = grad if grad is not None else torch.empty(self.P + 2, device=dev,
+                                                              dtype=torch.float32)
+        self._ws = torch.empty(max(nws, 256), dtype=torch.uint8, device=dev)
+        o = self.fwd.out
+        w = params.abi()
+        self._fn = lib.g2k_train_step_f32
+        self._head = (ctypes.byref(d), ctypes.byref(w), _ptr(pos), _ptr(vislet), _ptr(G),
+                      _ptr(targets), _ptr(n_active), _ptr(n_frames), _ptr(ped_mask), _ptr(h),
+                      _ptr(o.h), _ptr(o.pred), _ptr(o.metrics), ctypes.c_float(lam),
+                      self.grad.data_ptr(), self._ws.data_ptr(), nws)
+        self._stream = _stream(stream)
+        self._keep = (d, w, params, pos, vislet, G, targets, n_active, n_frames, ped_mask, h)
 
     @property
     def out(self):
         return self.fwd.out
 
-    def run(self) -> torch.Tensor:
+    def run(self, flat=None, ms=None, *, lr=LEARNING_RATE, decay=DECAY_RATE,
+            grad_clip=GRAD_CLIP) -> torch.Tensor:
+        """One call: outputs + grad; with ``flat`` also the update of the flat
+        parameters (and ``ms``: RMSProp, else SGD).  Returns grad [P + 2]."""
+        rc = self._fn(*self._head, None if flat is None else flat.data_ptr(),
+                      None if ms is None else ms.data_ptr(), float(lr), float(decay),
+                      float(grad_clip), self._stream)
+        if rc:
+            _lib.check("g2k_train_step_f32", rc)
+        return self.grad
+
+
+class TrainStep:
+    """One train-mode step over fixed device buffers: the fused reference
+    step (pred, h, ADE/FDE sums) and the loss gradient in one launch, the
+    all-reduce of the flat gradient across ranks (when a process group is
+    up), the update.  One rank: a single C call (g2k_train_step_f32 with the
+    update).
+
+    More input batches (same shapes, other buffers) can be bound with
+    ``bind``; ``run(slot)`` steps on batch ``slot`` with the shared
+    parameters and optimizer state.  The RMSProp mean squares start at one,
+    as TF's RMSPropOptimizer initialises its "rms" slot."""
+
+    kernel_names = "g2k_scene_kernel<GRAD> + g2k_grad_rows_kernel + g2k_update_kernel"
+
+    def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
+                 lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,
+                 n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None):
+        self.flat, self.params = flat_params(params)
+        self.P = self.flat.numel()
+        self.ms = torch.ones_like(self.flat) if rmsprop else None
+        self.lr, self.decay, self.grad_clip = lr, decay, grad_clip
+        self.group = group
+        self.world = (dist.get_world_size(group)
+                      if dist.is_available() and dist.is_initialized() else 1)
+        self._lam, self._stride = lam, stride
+        self._slots = []
+        self.bind(pos, vislet, G, targets, n_active, h, n_frames=n_frames, ped_mask=ped_mask,
+                  out=out)
+
+    def bind(self, pos, vislet, G, targets, n_active, h, *, n_frames=None, ped_mask=None,
+             out=None) -> int:
+        """Bind another input batch; returns its slot for ``run``."""
+        self._slots.append(TrainPlan(self.params, pos, vislet, G, targets, n_active, h,
+                                     n_frames=n_frames, ped_mask=ped_mask, stride=self._stride,
+                                     lam=self._lam, out=out))
+        return len(self._slots) - 1
+
+    @property
+    def out(self):
+        return self._slots[0].out
+
+    def outputs(self, slot=0):
+        return self._slots[slot].out
+
+    def run(self, slot=0) -> torch.Tensor:
         """Returns the (all-rank) [P + 2] buffer: gradient sums, loss, count."""
-        self.fwd.run()
-        if self.world == 1:                            # nothing to all-reduce: fused update
-            return self.gradplan.run_update(self.flat, self.ms, lr=self.lr, decay=self.decay,
-                                            grad_clip=self.grad_clip)
-        g = self.gradplan.run()
-        if self.world > 1:
-            allreduce_grad(g, self.group)
-        optimizer_update(self.flat, g, lr=self.lr, decay=self.decay, grad_clip=self.grad_clip,
-                         ms=self.ms)
+        plan = self._slots[slot]
+        kw = dict(lr=self.lr, decay=self.decay, grad_clip=self.grad_clip)
+        if self.world == 1:                            # nothing to all-reduce: update in the call
+            return plan.run(self.flat, self.ms, **kw)
+        g = plan.run()
+        allreduce_grad(g, self.group)
+        optimizer_update(self.flat, g, ms=self.ms, **kw)
         return g

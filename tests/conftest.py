@@ -22,6 +22,16 @@ def close(got, ref, tol=1e-4):
     return float(err.max()) if err.size else 0.0
 
 
+def close_h(got, ref, rtol=1e-5, atol=1e-8):
+    """The hidden state (rows of As @ softmax(h) sum to one, so entries are
+    ~1/H): |got - ref| <= rtol * |ref| + atol, every entry."""
+    import numpy as np
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    return bool(np.all(np.abs(got - ref) <= rtol * np.abs(ref) + atol))
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import torch

@@ -36,6 +36,7 @@ def _dims(**kw):
 
 
 @pytest.mark.parametrize("bad,code", [(dict(T=10), -4), (dict(D=10), -4), (dict(H=96), -4),
+                                      (dict(H=384), -4),
                                       (dict(Nmax=0), -1), (dict(Nmax=300), -1), (dict(W=26), -1),
                                       (dict(stride=-1), -1), (dict(S=-1), -1)])
 def test_step_rejects_bad_geometry(bad, code):
@@ -48,18 +49,17 @@ def test_step_rejects_bad_geometry(bad, code):
     assert lib.g2k_last_error()
 
 
-def test_step_rejects_null_and_small_workspace():
+def test_step_rejects_null_and_needs_no_workspace():
     lib = _lib.load()
     w = _lib.G2KWeights(*([ctypes.c_void_p(16)] * 7))
     p = ctypes.c_void_p(16)
     rc = lib.g2k_step_fused_f32(ctypes.byref(_dims()), ctypes.byref(w), None, p, p, p, p, None,
                                 None, p, p, p, p, None, None, 5e-4, p, 1 << 30, None)
     assert rc == -1
-    need = lib.g2k_step_workspace_bytes(ctypes.byref(_dims()))
-    assert need == 2 * 20 * 256 * 4 + 2 * 5 * 8 * 4
-    rc = lib.g2k_step_fused_f32(ctypes.byref(_dims()), ctypes.byref(w), p, p, p, p, p, None,
-                                None, p, p, p, p, None, None, 5e-4, p, need - 4, None)
-    assert rc == -1 and b"workspace" in lib.g2k_last_error()
+    # every intermediate of the fused step stays on chip
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims())) == 0
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims(T=9))) == -1
+    assert 0 < lib.g2k_step_lds_bytes(ctypes.byref(_dims())) <= 160 * 1024
 
 
 def test_other_entry_points_validate():
@@ -95,10 +95,9 @@ def test_gridlstm_and_train_entry_points_validate():
     d = _dims()
     assert lib.g2k_grad_size(ctypes.byref(d)) == 24 * 32 + 496
     need = lib.g2k_grad_workspace_bytes(ctypes.byref(d))
-    # (S x groups + 32 reduction slices) partial rows of P + 2 floats; the
-    # launcher picks 1..F frames per group (S = 2 here: one frame per group)
-    rows, rem = divmod(need, (24 * 32 + 498) * 4)
-    assert rem == 0 and 2 * 1 + 32 <= rows <= 2 * 20 + 32
+    # one gradient row [P + 2] per scene (the fused kernel's output)
+    assert need == 2 * (24 * 32 + 498) * 4
+    assert lib.g2k_train_workspace_bytes(ctypes.byref(d)) == need
     w = _lib.G2KWeights(*([p] * 7))
     rc = lib.g2k_step_grad_f32(ctypes.byref(d), ctypes.byref(w), p, p, p, p, p, None, None, 5e-4,
                                p, p, need - 4, None)
@@ -115,6 +114,32 @@ def test_gridlstm_and_train_entry_points_validate():
                                       5e-4, p, p, need - 4, p, None, 5e-3, 0.95, 10.0, None)
     assert rc == -1 and b"workspace" in lib.g2k_last_error()
     assert lib.g2k_update_f32(p, None, p, 0, 0.1, 0.9, 10.0, None) == 0
+    # g2k_train_step_f32(d, w, pos, vis, G, tgt, nact, nfr, mask, h_in, h_out, pred, met, lam,
+    #                    grad, ws, ws_bytes, params, ms, lr, decay, clip, stream)
+    rc = lib.g2k_train_step_f32(ctypes.byref(d), ctypes.byref(w), p, p, p, p, p, None, None, p, p,
+                                p, p, 5e-4, p, p, need - 4, None, None, 5e-3, 0.95, 10.0, None)
+    assert rc == -1 and b"workspace" in lib.g2k_last_error()
+    rc = lib.g2k_train_step_f32(ctypes.byref(d), ctypes.byref(w), p, p, p, p, p, None, None, None,
+                                p, p, p, 5e-4, p, p, need, None, None, 5e-3, 0.95, 10.0, None)
+    assert rc == -1
+    rc = lib.g2k_train_step_f32(ctypes.byref(_dims(H=96)), ctypes.byref(w), p, p, p, p, p, None,
+                                None, p, p, p, p, 5e-4, p, p, need, None, None, 5e-3, 0.95, 10.0,
+                                None)
+    assert rc == -4
+
+
+def test_small_D_entry_points():
+    """D in 1..16 for the class-level forward, the recurrence and the errors
+    (sample.py's num_freq_blocks = 10); the fused step needs D = 16."""
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)
+    w = _lib.G2KWeights(*([p] * 7))
+    assert lib.g2k_frame_recurrence_f32(ctypes.byref(_dims(D=17)), p, p, 3, None) == -4
+    assert lib.g2k_frame_recurrence_f32(ctypes.byref(_dims(D=10, S=0)), p, p, 3, None) == 0
+    assert lib.g2k_mcr_forward_f32(ctypes.byref(_dims(D=0)), ctypes.byref(w), p, p, p, p, p, p, p,
+                                   5e-4, None) == -4
+    assert lib.g2k_mcr_forward_f32(ctypes.byref(_dims(D=10, S=0)), ctypes.byref(w), p, p, p, p, p,
+                                   p, p, 5e-4, None) == 0
 
 
 def test_context_conv_validates():

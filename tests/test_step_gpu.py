@@ -1,5 +1,7 @@
 """GPU parity: the fused HIP step vs the float64 oracle (oracle/g2k_ref.py).
-Tolerance (written here): |got - ref| <= 1e-4 * max(1, |ref|)."""
+Tolerances (written here): pred and the metric sums
+|got - ref| <= 1e-4 * max(1, |ref|); the hidden state h (entries ~1/H) is held
+relatively, |got - ref| <= 1e-5 * |ref| + 1e-8 (close_h)."""
 import numpy as np
 import pytest
 import torch
@@ -7,7 +9,8 @@ import torch
 from multimodaltraj_2_amd import frame_step as fs
 from multimodaltraj_2_amd.synthetic import make_batch
 from oracle import g2k_ref as ref
-from tests.conftest import close
+from multimodaltraj_2_amd.synthetic import CONFIGS
+from tests.conftest import close, close_h
 
 TOL = 1e-4
 pytestmark = pytest.mark.gpu
@@ -56,7 +59,7 @@ def test_step_matches_oracle(gpu, S, Nmax, H):
         A_ref = np.stack(ex["A"])
         assert np.abs(attn[s] - A_ref).max() <= TOL * max(1.0, np.abs(A_ref).max())
         assert close(cost[s], np.stack(ex["cost"])) <= TOL
-        assert close(hh[s], h) <= TOL
+        assert close_h(hh[s], h)
         assert close(met[s, :6], m[:6]) <= TOL
 
 
@@ -75,7 +78,7 @@ def test_step_large_logits(gpu):
         assert np.abs(A_ref).max() > 87.0
         assert np.abs(attn[s] - A_ref).max() <= TOL * max(1.0, np.abs(A_ref).max())
         assert close(pred[s, :, :, :n].reshape(12, 2, 12, n), pr) <= TOL
-        assert close(hh[s], h) <= TOL
+        assert close_h(hh[s], h)
 
 
 def test_step_nonzero_h0_and_masks(gpu):
@@ -93,7 +96,7 @@ def test_step_nonzero_h0_and_masks(gpu):
         nf = pr.shape[0]
         assert close(pred[s, :nf, :, :n].reshape(nf, 2, 12, n), pr) <= TOL
         assert np.all(pred[s, nf:] == 0)
-        assert close(hh[s], h) <= TOL
+        assert close_h(hh[s], h)
         assert close(met[s, :6], m[:6]) <= TOL
 
 
@@ -145,7 +148,7 @@ def test_recurrence_matches_oracle(gpu):
         hr = h0[s].astype(np.float64)
         for f in range(F):
             hr = ref.recurrence_step(A[s, f].astype(np.float64), hr)
-        assert close(got[s], hr) <= TOL
+        assert close_h(got[s], hr)
 
 
 def test_ade_fde_variants(gpu):
@@ -189,7 +192,7 @@ def _check_all(b, out, res, S):
         nf = pr.shape[0]
         assert close(pred[s, :nf, :, :n].reshape(nf, 2, 12, n), pr) <= TOL
         assert np.all(pred[s, :, :, n:] == 0)
-        assert close(hh[s], h) <= TOL
+        assert close_h(hh[s], h)
         assert close(met[s, :6], m[:6]) <= TOL
 
 
@@ -204,27 +207,33 @@ def test_step_fallbacks_and_chunks(gpu, S, Nmax, H, F):
     _check_all(b, out, res, S)
 
 
-@pytest.mark.parametrize("env,val", [("G2K_DMA16", "1"), ("G2K_STEP_SPLIT", "1"),
-                                     ("G2K_SCENE_OPTS", "1"), ("G2K_SCENE_OPTS", "2"),
-                                     ("G2K_SCENE_OPTS", "3")])
-def test_step_paths_agree(gpu, monkeypatch, env, val):
-    """The 16-B and the 4-byte LDS-DMA staging move the same bytes, so they
-    must agree bitwise; the two-kernel split and the scene-kernel options
-    (recurrence-wave heads, VALU prediction tiles) sum in another order and
-    are held to the parity tolerance."""
-    b = make_batch(4, 32, 128, seed=9)
-    params = fs.init_params(32, seed=0, device=gpu)
+# BASELINE.json configs at their own benchmark shapes (bench.py rank 0
+# batch): every 16th scene in full (pred, h, metrics) and the metric sums
+# over all scenes.  cfg 5 (Nmax 256, H 256) is the LDS-chunked layout.
+CFG = [("eth_hotel_synth", 256), ("eth_ucy_loo_kfold4", 128), ("relational_attn_h256", 256),
+       ("dense_crowd", 128)]
+
+
+@pytest.mark.parametrize("name,S", CFG)
+def test_config_shape_matches_oracle(gpu, name, S):
+    c = CONFIGS[name]
+    Nmax, H = c["Nmax"], c["H"]
+    b = make_batch(S, Nmax, H, seed=1)
+    params = fs.init_params(Nmax, seed=0, device=gpu)
     t = b.to_device(gpu)
-    args = (params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
-    o1 = fs.step_fused(*args)
+    out = fs.step_fused(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
+                        t["h0"])
     torch.cuda.synchronize()
-    monkeypatch.setenv(env, val)
-    o2 = fs.step_fused(*args)
-    torch.cuda.synchronize()
-    if env == "G2K_DMA16":
-        assert torch.equal(o1.pred, o2.pred)
-        assert torch.equal(o1.h, o2.h)
-        assert torch.equal(o1.metrics, o2.metrics)
-    else:
-        assert close(o2.pred.cpu().numpy(), o1.pred.cpu().numpy()) <= TOL
-        assert close(o2.h.cpu().numpy(), o1.h.cpu().numpy()) <= TOL
+    pred, hh, met = out.pred.cpu().numpy(), out.h.cpu().numpy(), out.metrics.cpu().numpy()
+    w = params.numpy()
+    tot = np.zeros(6)
+    for s in range(S):
+        pr, h, m, _ = ref.scene_step(b.pos[s], b.vislet[s], b.G[s], w, b.targets[s],
+                                     b.n_active[s], b.h0[s], n_frames=b.F)
+        tot += m[:6]
+        if s % 16 == 0 or s == S - 1:
+            n = int(b.n_active[s])
+            assert close(pred[s, :, :, :n].reshape(b.F, 2, 12, n), pr) <= TOL, s
+            assert close_h(hh[s], h), s
+            assert close(met[s, :6], m[:6]) <= TOL, s
+    assert close(met[:, :6].astype(np.float64).sum(axis=0), tot) <= TOL

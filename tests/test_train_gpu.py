@@ -10,8 +10,9 @@ import torch
 
 from multimodaltraj_2_amd import frame_step as fs
 from multimodaltraj_2_amd import train_step as ts
-from multimodaltraj_2_amd.synthetic import make_batch
+from multimodaltraj_2_amd.synthetic import CONFIGS, make_batch
 from oracle import g2k_ref as ref
+from tests.conftest import close
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
@@ -31,18 +32,13 @@ def _ref_grad(b, w, nfr, mask, lam):
     return loss, cnt, R
 
 
-# G2K_GRAD_FPG forces frames per workgroup (the launcher picks 1 for these
-# small S): groups of 2/3/8 frames exercise the prefetch double buffer, the
-# frame-order row accumulation and n_frames ending inside a group;
-# G2K_GRAD_GW selects the one-wave-per-frame kernel
-@pytest.mark.parametrize("Nmax,F,lam,env", [
-    (32, 6, 5e-4, {}), (7, 5, 0.05, {}), (200, 3, 0.05, {}),
-    (32, 7, 0.05, {"G2K_GRAD_FPG": "3"}), (20, 9, 0.05, {"G2K_GRAD_FPG": "2"}),
-    (64, 7, 5e-4, {"G2K_GRAD_FPG": "8"}), (256, 4, 0.05, {"G2K_GRAD_FPG": "3"}),
-    (32, 6, 5e-4, {"G2K_GRAD_GW": "4"}), (200, 3, 0.05, {"G2K_GRAD_GW": "2"})])
-def test_grad_matches_oracle(gpu, monkeypatch, Nmax, F, lam, env):
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+# Nmax 7 / 20 / 30: partial pedestrian tiles; Nmax 200 / 256: the dWo
+# accumulation in frame order (one copy) instead of one copy per producer;
+# F 40: two frame chunks
+@pytest.mark.parametrize("Nmax,F,lam", [
+    (32, 6, 5e-4), (7, 5, 0.05), (200, 3, 0.05), (32, 7, 0.05), (20, 9, 0.05), (64, 7, 5e-4),
+    (256, 4, 0.05), (30, 40, 0.05)])
+def test_grad_matches_oracle(gpu, Nmax, F, lam):
     S = 3
     b = make_batch(S, Nmax, 64, F=F, seed=21)
     mask = np.ones((S, Nmax), bool)
@@ -55,6 +51,10 @@ def test_grad_matches_oracle(gpu, monkeypatch, Nmax, F, lam, env):
                      ped_mask=torch.from_numpy(mask.astype(np.uint8)).to(gpu), lam=lam)
     g = gp.run().cpu().numpy().astype(np.float64)
     loss, cnt, R = _ref_grad(b, params.numpy(), nfr, mask, lam)
+    _check_grad(g, loss, cnt, R, Nmax)
+
+
+def _check_grad(g, loss, cnt, R, Nmax):
     P = ts.grad_size(Nmax)
     assert g.shape == (P + 2,)
     off = 0
@@ -142,3 +142,92 @@ def test_train_step_reduces_loss(gpu):
     assert losses[-1] < losses[0]
     # the step's forward outputs are the reference-mode step on the updated weights
     assert torch.isfinite(step.out.pred).all() and torch.isfinite(step.out.h).all()
+
+
+def _train_batch(gpu, S, Nmax, H, F=20, seed=3):
+    b = make_batch(S, Nmax, H, F=F, seed=seed, h0_scale=1.0)
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    return b, params, b.to_device(gpu)
+
+
+def test_train_step_outputs_match_forward_step(gpu):
+    """g2k_train_step_f32: its pred / h are the reference-mode step's bit for
+    bit (same tiles, same recurrence); the metric sums the same within the
+    tolerance (the train kernel's producers own whole frames, so the sums
+    run in another order); its gradient is g2k_step_grad_f32's bit for bit."""
+    b, params, t = _train_batch(gpu, 6, 32, 128)
+    args = (params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+    o1 = fs.step_fused(*args)
+    tp = ts.TrainPlan(*args)
+    g = tp.run().clone()
+    g2 = ts.GradPlan(*args[:6]).run().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(o1.pred, tp.out.pred)
+    assert torch.equal(o1.h, tp.out.h)
+    assert close(tp.out.metrics.cpu().numpy(), o1.metrics.cpu().numpy()) <= TOL
+    assert torch.equal(g, g2)
+
+
+@pytest.mark.parametrize("name,S", [("eth_hotel_synth", 256), ("eth_ucy_loo_kfold4", 128),
+                                    ("relational_attn_h256", 256), ("dense_crowd", 128)])
+def test_train_config_shape_matches_oracle(gpu, name, S):
+    """The loss gradient at each BASELINE config's benchmark shape: the
+    all-scene sum [P + 2] against the oracle's, and every 16th scene's own
+    gradient row (the workspace rows the sum is formed from)."""
+    c = CONFIGS[name]
+    Nmax, H = c["Nmax"], c["H"]
+    b, params, t = _train_batch(gpu, S, Nmax, H, seed=1)
+    tp = ts.TrainPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+    g = tp.run().cpu().numpy().astype(np.float64)
+    torch.cuda.synchronize()
+    P = ts.grad_size(Nmax)
+    rows = tp._ws[:S * (P + 2) * 4].view(torch.float32).reshape(S, P + 2).cpu().numpy()
+    w = params.numpy()
+    R = {k: np.zeros(np.shape(w[k])) for k in ref.GRAD_ORDER}
+    loss = cnt = 0
+    for s in range(S):
+        l, cn, gs = ref.scene_loss_grad(b.pos[s], b.vislet[s], b.G[s], w, b.targets[s],
+                                        b.n_active[s], n_frames=b.F)
+        loss += l
+        cnt += cn
+        for k in R:
+            R[k] += gs[k]
+        if s % 16 == 0:
+            r = np.concatenate([np.asarray(gs[k]).reshape(-1) for k in ref.GRAD_ORDER])
+            assert np.abs(rows[s, :P] - r).max() <= TOL * np.abs(r).max(), s
+            assert abs(rows[s, P] - l) <= TOL * l and rows[s, P + 1] == cn
+    _check_grad(g, loss, cnt, R, Nmax)
+
+
+def test_train_step_world2_branch_matches_one_rank(gpu, monkeypatch):
+    """TrainStep's multi-rank branch (gradient, all-reduce, separate update)
+    driven on one GPU: with the all-reduce of a one-rank group (identity) it
+    must give the one-call update bit for bit; with the scenes split into two
+    halves and their gradients summed (what the all-reduce of two ranks
+    does) the update agrees within the tolerance."""
+    b, params, t = _train_batch(gpu, 8, 32, 128)
+    keys = ("pos", "vislet", "G", "targets", "n_active", "h0")
+    one = ts.TrainStep(params, *(t[k] for k in keys))
+    g1 = one.run().clone()
+    p1 = one.flat.clone()
+    two = ts.TrainStep(params, *(t[k] for k in keys))
+    two.world = 2
+    monkeypatch.setattr(ts, "allreduce_grad", lambda buf, group=None: buf)
+    g2 = two.run().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(g1, g2) and torch.equal(p1, two.flat)
+    # two halves, gradients summed as the all-reduce would, one update
+    flat, views = ts.flat_params(params)
+    ms = torch.ones_like(flat)
+    gs = []
+    for lo, hi in ((0, 4), (4, 8)):
+        h = {k: t[k][lo:hi].contiguous() for k in keys}
+        gs.append(ts.TrainPlan(views, *(h[k] for k in keys)).run().clone())
+    gsum = gs[0] + gs[1]
+    ts.optimizer_update(flat, gsum, ms=ms)
+    torch.cuda.synchronize()
+    P = flat.numel()
+    gn, gr = gsum.cpu().numpy(), g1.cpu().numpy()
+    assert np.abs(gn[:P] - gr[:P]).max() <= 1e-5 * np.abs(gr[:P]).max()
+    assert gn[P + 1] == gr[P + 1]
+    assert np.abs(flat.cpu().numpy() - p1.cpu().numpy()).max() <= 1e-5
