@@ -46,9 +46,10 @@ constexpr int SM_K2 = 752;
 constexpr int kSceneSmall = 1088;
 constexpr int kKA = 12;       // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
 // train mode
-constexpr int kGFrame = 832;  // per-producer frame scratch: dM [24][8], dcost [8][8], dE [8][16],
-                              // terms: dWc_f [24][8], dK1_f [8][10], dUaug_f [11][16]
-constexpr int kGT_DM = 0, kGT_DC = 192, kGT_DE = 256, kGT_TERMS = 384, kGTerms = 448;
+constexpr int kGFrame = 384;  // per-producer frame scratch: dM [24][8], dcost [8][8], dE [8][16]
+constexpr int kGT_DM = 0, kGT_DC = 192, kGT_DE = 256;
+constexpr int kGTerms = 448;  // one frame's terms (ring slot): dWc_f [24][8], dK1_f [8][10],
+                              // dUaug_f [11][16]
 constexpr int kGAccFixed = 320;   // dWc [24][8], dK1 [8][10], dVe [2][16], dbv [16]
 constexpr int kGA_WC = 0, kGA_K1 = 192, kGA_VE = 272, kGA_BV = 304;
 
@@ -59,7 +60,7 @@ struct SceneLayout {
   // train mode (zero-sized otherwise)
   int wtot;            // window rows of the whole scene ((F - 1) * stride + T)
   int dwo_seq;         // 1: dWo^T accumulated in frame order (one copy); 0: one copy per producer
-  int o_cost, o_gframe, o_gacc, o_gdv, o_gdwo, o_gseq;
+  int o_cost, o_gframe, o_gring, o_gacc, o_gdv, o_gdwo, o_gseq;
   int total;           // floats
 };
 
@@ -86,14 +87,15 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_vg = o;    o += rup4((s.wcmax + 3) * kT);       // VG = V @ g: window, Ve0, Ve1, bv rows
   s.wtot = (F > 0 ? F - 1 : 0) * stride + kT;
   s.dwo_seq = (int64_t)NP * Nmax * kT * 4 > 32 * 1024 ? 1 : 0;
-  s.o_cost = s.o_gframe = s.o_gacc = s.o_gdv = s.o_gdwo = s.o_gseq = o;
+  s.o_cost = s.o_gframe = s.o_gring = s.o_gacc = s.o_gdv = s.o_gdwo = s.o_gseq = o;
   if (grad) {
     s.o_cost = o;   o += fc * kT * kT;                 // cost_f per chunk frame (head -> terms)
     s.o_gframe = o; o += NP * kGFrame;
+    s.o_gring = o;  o += fc * kGTerms;                 // the chunk's frame terms, summed at its end
     s.o_gacc = o;   o += kGAccFixed;
     s.o_gdv = o;    o += rup4(s.wtot * kD);            // dV: window-row gradient [wtot][16]
     s.o_gdwo = o;   o += (s.dwo_seq ? 1 : NP) * Nmax * kT;   // dWo^T [Nmax][8]
-    s.o_gseq = o;   o += rup4(2 + (Nmax + 15) / 16);   // frame seq, done count, tile seqs
+    s.o_gseq = o;   o += rup4(2 + (Nmax + 15) / 16);   // chunk count, -, dWo tile seqs
   }
   s.total = o;
   return s;
@@ -207,19 +209,42 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
                                                    const float (&rm)[4], float lam, float* as_dst,
                                                    float* A_g, float* cost_g, float* cost_l, int L,
                                                    int q) {
-  float ka[3], ua[3], va[3];
+  // every operand load is unconditional (clamped addresses) and issued
+  // before the first MFMA; the lanes' selects follow (an exec-masked load
+  // would cost its own LDS round trip on the chain)
+  const int L7 = L & 7, Lx = L < kL ? L : 0, q2 = q < 2 ? q : 1;
+  float ka[3], ua[3], va[3], bx[3], by[3], gA[4], ub, vb;
 #pragma unroll
   for (int ks = 0; ks < 3; ++ks) {
     const int k = 4 * ks + q;
-    ka[ks] = L < kT ? sm[SM_K1 + L * kKA + k] : 0.f;
+    ka[ks] = sm[SM_K1 + L7 * kKA + k];
+    bx[ks] = sm[SM_K2 + Lx * kKA + k];
+    by[ks] = sm[SM_K2 + (kL + Lx) * kKA + k];
     if (ks < 2) {
       ua[ks] = sV[(wrow0 + k) * kD + L];
-      va[ks] = L < kT ? sVG[(wrow0 + k) * kT + L] : 0.f;
+      va[ks] = sVG[(wrow0 + k) * kT + L7];
     } else {
-      ua[ks] = q < 2 ? sV[(wcmax + q) * kD + L] : (q == 2 ? sm[SM_BV + L] : 0.f);
-      va[ks] = L >= kT || q == 3 ? 0.f : sVG[(wcmax + q) * kT + L];   // Ve0, Ve1, bv rows
+      ua[ks] = sV[(wcmax + q2) * kD + L];
+      va[ks] = sVG[(wcmax + (q < 3 ? q : 2)) * kT + L7];   // Ve0, Ve1, bv rows
     }
   }
+  ub = sm[SM_BV + L];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) gA[ks] = sm[SM_G + L * kT + 4 * q2 + ks];   // g[r = L][t]
+  asm volatile("" : "+v"(ka[0]), "+v"(ka[1]), "+v"(ka[2]), "+v"(ua[0]), "+v"(ua[1]), "+v"(ua[2]),
+               "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(ub));
+  asm volatile("" : "+v"(bx[0]), "+v"(bx[1]), "+v"(bx[2]), "+v"(by[0]), "+v"(by[1]), "+v"(by[2]),
+               "+v"(gA[0]), "+v"(gA[1]), "+v"(gA[2]), "+v"(gA[3]));
+  (void)vb;
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    ka[ks] = L < kT ? ka[ks] : 0.f;
+    bx[ks] = L < kL ? bx[ks] : 0.f;
+    by[ks] = L < kL ? by[ks] : 0.f;
+    va[ks] = L < kT ? va[ks] : 0.f;
+  }
+  ua[2] = q < 2 ? ua[2] : (q == 2 ? ub : 0.f);
+  va[2] = q == 3 ? 0.f : va[2];
   f32x4 eN = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);          // E[4q+i][L]
@@ -228,11 +253,8 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
   o.mT1 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 3; ++ks) {
-    const int k = 4 * ks + q;
-    const float bx = L < kL ? sm[SM_K2 + L * kKA + k] : 0.f;
-    const float by = L < kL ? sm[SM_K2 + (kL + L) * kKA + k] : 0.f;
-    o.mT0 = mfma4(va[ks], bx, o.mT0);   // M[L][4q+i]       (x rows)
-    o.mT1 = mfma4(va[ks], by, o.mT1);   // M[12+L][4q+i]    (y rows)
+    o.mT0 = mfma4(va[ks], bx[ks], o.mT0);   // M[L][4q+i]       (x rows)
+    o.mT1 = mfma4(va[ks], by[ks], o.mT1);   // M[12+L][4q+i]    (y rows)
   }
   f32x4 aA = {0.f, 0.f, 0.f, 0.f};
   {
@@ -240,10 +262,8 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
 #pragma unroll
     for (int i = 0; i < 4; ++i) em[i] = eN[i] * rm[i];                    // rm = 0 for t >= 8
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const float gA = q < 2 ? lam * sm[SM_G + L * kT + 4 * q + ks] : 0.f;  // g[r = L][t]
-      aA = mfma4(gA, em[ks], aA);                                        // A[4q+i][L]
-    }
+    for (int ks = 0; ks < 4; ++ks)
+      aA = mfma4(q < 2 ? lam * gA[ks] : 0.f, em[ks], aA);                 // A[4q+i][L]
   }
   if (A_g) {
 #pragma unroll
@@ -268,11 +288,12 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
 // Per-workgroup context of the scene kernel (LDS carve-up, scene scalars).
 struct SceneCtx {
   float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sPos, *sVG, *sY;
-  float *sCost, *sGFrame, *sGAcc, *sGdV, *sGdWo;
+  float *sCost, *sGFrame, *sGRing, *sGAcc, *sGdV, *sGdWo;
   int* sFlag;     // As ring: global frame + 1 once the frame's As is in its slot
   int* sMflag;    // M ring: global frame + 1 once the frame's M is in its slot
   int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
-  int* sGseq;     // train: [0] frames added, [1] unused, [2 + t] frames added to dWo tile t
+  int* sGseq;     // train: [0] producers done with the chunk's frames (cumulative), [2 + t]
+                  // frames added to dWo tile t (dwo_seq)
   int s, tid, lane, wv, L, q, nact, nf, ntiles, ntact;
 };
 
@@ -532,14 +553,24 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
   const int ne = n0 + pp;
   const bool has_t = ne < nact && (pm ? pm[ne] != 0 : true);
   f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
+  {
+    // unconditional loads at clamped addresses, selects after (see frame_head)
+    const int n = n0 + L, nc = n < Nmax ? n : Nmax - 1, Lx = L < kL ? L : 0;
+    float wo[2], bx[2], by[2];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int n = n0 + L, k = 4 * ks + q;
-    const float wo = n < nact ? sWo[k * Nmax + n] : 0.f;
-    const float bx = L < kL ? M[L * kT + k] : 0.f;
-    const float by = L < kL ? M[(kL + L) * kT + k] : 0.f;
-    y0 = mfma4(wo, bx, y0);   // Y[L][n0 + 4q + i]
-    y1 = mfma4(wo, by, y1);   // Y[12 + L][n0 + 4q + i]
+    for (int ks = 0; ks < 2; ++ks) {
+      const int k = 4 * ks + q;
+      wo[ks] = sWo[k * Nmax + nc];
+      bx[ks] = M[Lx * kT + k];
+      by[ks] = M[(kL + Lx) * kT + k];
+    }
+    asm volatile("" : "+v"(wo[0]), "+v"(wo[1]), "+v"(bx[0]), "+v"(bx[1]), "+v"(by[0]), "+v"(by[1]));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const float w = n < nact ? wo[ks] : 0.f;
+      y0 = mfma4(w, L < kL ? bx[ks] : 0.f, y0);   // Y[L][n0 + 4q + i]
+      y1 = mfma4(w, L < kL ? by[ks] : 0.f, y1);   // Y[12 + L][n0 + 4q + i]
+    }
   }
   if (L < kL) {
     const int nb = n0 + 4 * q;
@@ -607,10 +638,19 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
       for (int ks = 0; ks < 4; ++ks) {
         const int k = 4 * q + ks;
         const float2 d = *reinterpret_cast<const float2*>(ys + k * kL2 + 2 * (L < kL ? L : 0));
-        ax[ks] = L < kL ? d.x : 0.f;
-        ay[ks] = L < kL ? d.y : 0.f;
+        ax[ks] = d.x;
+        ay[ks] = d.y;
         const int n = n0 + k;
-        bw[ks] = (L < kT && n < nact) ? sWo[(L & 7) * Nmax + (n < Nmax ? n : 0)] : 0.f;
+        bw[ks] = sWo[(L & 7) * Nmax + (n < Nmax ? n : 0)];
+      }
+      asm volatile("" : "+v"(ax[0]), "+v"(ax[1]), "+v"(ax[2]), "+v"(ax[3]), "+v"(ay[0]), "+v"(ay[1]),
+                   "+v"(ay[2]), "+v"(ay[3]), "+v"(bw[0]), "+v"(bw[1]), "+v"(bw[2]), "+v"(bw[3]));
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int n = n0 + 4 * q + ks;
+        ax[ks] = L < kL ? ax[ks] : 0.f;
+        ay[ks] = L < kL ? ay[ks] : 0.f;
+        bw[ks] = (L < kT && n < nact) ? bw[ks] : 0.f;
       }
       f32x4 mx = {0.f, 0.f, 0.f, 0.f}, my = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -635,8 +675,12 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
         const int r = 4 * ks + q;
         const int col = r < kL ? 2 * r : 2 * (r - kL) + 1;
         ar[ks] = ys[L * kL2 + col];
-        br[ks] = L < kT ? M[r * kT + (L & 7)] : 0.f;
+        br[ks] = M[r * kT + (L & 7)];
       }
+      asm volatile("" : "+v"(ar[0]), "+v"(ar[1]), "+v"(ar[2]), "+v"(ar[3]), "+v"(ar[4]), "+v"(ar[5]),
+                   "+v"(br[0]), "+v"(br[1]), "+v"(br[2]), "+v"(br[3]), "+v"(br[4]), "+v"(br[5]));
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) br[ks] = L < kT ? br[ks] : 0.f;
       f32x4 w = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) w = mfma4(ar[ks], br[ks], w);
@@ -656,95 +700,147 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Wait (one LDS word, wave-uniform) until *w == want.
 __device__ __forceinline__ void poll_word(const int* w, int want) { poll_flag(w, want); }
 
-// GRAD, after the last tile of frame f (chunk slot fl): the frame's
-// weight-side terms on the VALU of this wave (one lane per output entry),
-// then their addition into the scene's accumulators in frame order.
+// D = A @ B on one 16 x 16 tile by v_mfma_f32_16x16x4_f32 with k = 4 ks + q:
+// lane (L, q) supplies A(L, k) and B(k, L) at k-step ks (the functors load
+// unconditionally at clamped LDS addresses and select), every load issued
+// before the first MFMA; the result lands as D(4q + v, L) in register v.
+template <int KS, typename FA, typename FB>
+__device__ __forceinline__ f32x4 mm16(FA fa, FB fb, int L, int q) {
+  float av[KS], bv[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    av[ks] = fa(L, 4 * ks + q);
+    bv[ks] = fb(4 * ks + q, L);
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) acc = mfma4(av[ks], bv[ks], acc);
+  return acc;
+}
+
+// GRAD, after the last tile of chunk frame fl: the frame's weight-side
+// terms (one wave, MFMA tiles from LDS) into the chunk's ring slot fl;
+// grad_chunk_sum adds the slots in frame order.
 //   dcost[u][t] = sum_r Wc[r][u] dM[r][t]          (M = Wc @ cost, :119)
 //   dE[t][d]    = lambda sum_u dcost[t][u] G[d][u] (cost = E @ g, :112-113)
 //   dWc_f[r][u] = sum_t dM[r][t] cost[u][t]
 //   dK1_f[t][j] = sum_d dE[t][d] Uaug[j][d]        (E = K1 @ Uaug, j < 10)
 //   dUaug_f[j][d] = sum_t K1[t][j] dE[t][d]        (j < 8: window rows, 8-9: Ve, 10: bv)
 __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout& lay,
-                                           const SceneCtx& c, int fb, int fl) {
+                                           const SceneCtx& c, int fl) {
   float* gf = c.sGFrame + (c.wv - kRecW) * kGFrame;
   float* dM = gf + kGT_DM;
   float* dC = gf + kGT_DC;
   float* dE = gf + kGT_DE;
-  float* tm = gf + kGT_TERMS;
+  float* tm = c.sGRing + fl * kGTerms;
   const int L = c.L, q = c.q, lane = c.lane;
   const float* sm = c.sm;
-  (void)L; (void)q;
-  wave_lds_sync();                                        // the frame's dM, all tiles added
-  {
-    const int u = lane >> 3, tt = lane & 7;
-    float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < kL2; r += 2) {
-      s0 = fmaf(sm[SM_WC + r * kT + u], dM[r * kT + tt], s0);
-      s1 = fmaf(sm[SM_WC + (r + 1) * kT + u], dM[(r + 1) * kT + tt], s1);
-    }
-    dC[lane] = s0 + s1;
-  }
-  wave_lds_sync();
-#pragma unroll 1
-  for (int o = lane; o < kT * kD; o += 64) {
-    const int t = o >> 4, d = o & 15;
-    float s = 0.f;
-#pragma unroll
-    for (int u = 0; u < kT; ++u) s = fmaf(dC[t * kT + u], sm[SM_G + d * kT + u], s);
-    dE[o] = a.lambda * s;
-  }
-  wave_lds_sync();
   const float* cost = c.sCost + fl * kT * kT;
   const int wrow0 = fl * a.d.stride;
-#pragma unroll 1
-  for (int o = lane; o < kL2 * kT; o += 64) {             // dWc_f
-    const int r = o >> 3, u = o & 7;
-    float s = 0.f;
+  wave_lds_sync();                                        // the frame's dM, all tiles added
+  {                                                       // dcost: [8 u][8 t], K = 24 rows r
+    const f32x4 d = mm16<6>(
+        [&](int i, int k) { const float x = sm[SM_WC + k * kT + (i & 7)]; return i < kT ? x : 0.f; },
+        [&](int k, int j) { const float x = dM[k * kT + (j & 7)]; return j < kT ? x : 0.f; }, L, q);
+    if (q < 2 && L < kT) {
 #pragma unroll
-    for (int t = 0; t < kT; ++t) s = fmaf(dM[r * kT + t], cost[u * kT + t], s);
-    tm[o] = s;
-  }
-  for (int o = lane; o < kT * 10; o += 64) {              // dK1_f
-    const int t = o / 10, j = o - t * 10;
-    const float* ur = c.sV + (j < kT ? wrow0 + j : lay.wcmax + (j - kT)) * kD;
-    float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-    for (int d = 0; d < kD; d += 2) {
-      s0 = fmaf(dE[t * kD + d], ur[d], s0);
-      s1 = fmaf(dE[t * kD + d + 1], ur[d + 1], s1);
+      for (int v = 0; v < 4; ++v) dC[(4 * q + v) * kT + L] = d[v];
     }
-    tm[kL2 * kT + o] = s0 + s1;
   }
-#pragma unroll 1
-  for (int o = lane; o < 11 * kD; o += 64) {              // dUaug_f
-    const int j = o >> 4, d = o & 15;
-    float s = 0.f;
+  wave_lds_sync();
+  {                                                       // dE: [8 t][16 d], K = 8 u
+    const f32x4 d = mm16<2>(
+        [&](int i, int k) { const float x = dC[(i & 7) * kT + k]; return i < kT ? x : 0.f; },
+        [&](int k, int j) { return sm[SM_G + j * kT + k]; }, L, q);
+    if (q < 2) {
 #pragma unroll
-    for (int t = 0; t < kT; ++t) s = fmaf(sm[SM_K1 + t * kKA + j], dE[t * kD + d], s);
-    tm[kL2 * kT + kT * 10 + o] = s;
+      for (int v = 0; v < 4; ++v) dE[(4 * q + v) * kD + L] = a.lambda * d[v];
+    }
+  }
+  {                                                       // dWc_f: [24 r][8 u], K = 8 t
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 d = mm16<2>(
+          [&](int i, int k) {
+            const int r = 16 * h + i;
+            const float x = dM[(r < kL2 ? r : 0) * kT + k];
+            return r < kL2 ? x : 0.f;
+          },
+          [&](int k, int j) { const float x = cost[(j & 7) * kT + k]; return j < kT ? x : 0.f; }, L, q);
+      if (L < kT) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int r = 16 * h + 4 * q + v;
+          if (r < kL2) tm[r * kT + L] = d[v];
+        }
+      }
+    }
+  }
+  wave_lds_sync();                                        // dE complete
+  {                                                       // dK1_f: [8 t][10 j], K = 16 d
+    const int jr = L < kT ? wrow0 + L : lay.wcmax + (L < kT + 2 ? L - kT : 1);   // Uaug row j = L
+    const f32x4 d = mm16<4>(
+        [&](int i, int k) { const float x = dE[(i & 7) * kD + k]; return i < kT ? x : 0.f; },
+        [&](int k, int j) { const float x = c.sV[jr * kD + k]; return j < kT + 2 ? x : 0.f; }, L, q);
+    if (q < 2 && L < kT + 2) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) tm[kL2 * kT + (4 * q + v) * 10 + L] = d[v];
+    }
+  }
+  {                                                       // dUaug_f: [11 j][16 d], K = 8 t
+    const f32x4 d = mm16<2>(
+        [&](int i, int k) { const float x = sm[SM_K1 + k * kKA + (i < kKA ? i : 0)]; return i < 11 ? x : 0.f; },
+        [&](int k, int j) { return dE[k * kD + j]; }, L, q);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int j = 4 * q + v;
+      if (j < 11) tm[kL2 * kT + kT * 10 + j * kD + L] = d[v];
+    }
   }
   wave_lds_sync();
   for (int o = lane; o < kL2 * kT; o += 64) dM[o] = 0.f;  // for this wave's next frame
-  const int f = fb + fl;
-  poll_word(c.sGseq, f);                                  // frames < f added
-  float* ga = c.sGAcc;
-#pragma unroll 1
-  for (int o = lane; o < kGTerms; o += 64) {
-    const float v = tm[o];
-    if (o < kL2 * kT) {
-      ga[kGA_WC + o] += v;
-    } else if (o < kL2 * kT + kT * 10) {
-      ga[kGA_K1 + o - kL2 * kT] += v;
+}
+
+// GRAD, once every producer is done with chunk [fb, fb + cnt): the ring's
+// frame terms added into the scene's accumulators, frame after frame
+// (deterministic), every accumulator entry by one producer lane: dWc, dK1,
+// dVe, dbv, and the window rows the chunk's frames touch (dV[f stride + j]
+// += dU_f[j]).
+__device__ __forceinline__ void grad_chunk_sum(const StepArgs& a, const SceneCtx& c, int fb,
+                                               int cnt, int NP) {
+  const int stride = a.d.stride;
+  const int nfix = kGAccFixed;                              // dWc, dK1, dVe, dbv
+  const int r0 = fb * stride, nrow = (cnt - 1) * stride + kT;   // window rows touched
+  const int ptid = (c.wv - kRecW) * 64 + c.lane;
+  for (int e = ptid; e < nfix + nrow * kD; e += NP * 64) {
+    // the entry's ring column per frame (-1: the frame does not touch it)
+    int col0 = -1, w = 0;
+    if (e < nfix) {
+      if (e < kGA_VE) col0 = e;                                                // dWc, dK1
+      else if (e < kGA_BV) col0 = kL2 * kT + kT * 10 + kT * kD + (e - kGA_VE);   // dUaug rows 8, 9
+      else col0 = kL2 * kT + kT * 10 + (kT + 2) * kD + (e - kGA_BV);           // dUaug row 10
     } else {
-      const int p = o - kL2 * kT - kT * 10, j = p >> 4, d = p & 15;
-      if (j < kT) c.sGdV[(f * a.d.stride + j) * kD + d] += v;
-      else if (j < kT + 2) ga[kGA_VE + (j - kT) * kD + d] += v;
-      else ga[kGA_BV + d] += v;
+      w = (e - nfix) >> 4;                                  // chunk-local window row
     }
+    const int d = (e - nfix) & 15;
+    float s = 0.f;
+    for (int f0 = 0; f0 < cnt; f0 += 8) {                   // eight frames' loads in flight
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int f = f0 + i;
+        const int j = w - f * stride;
+        const int col = e < nfix ? col0 : kL2 * kT + kT * 10 + (j >= 0 && j < kT ? j : 0) * kD + d;
+        v[i] = c.sGRing[(f < cnt ? f : 0) * kGTerms + col];
+        const bool on = f < cnt && (e < nfix || (j >= 0 && j < kT));
+        v[i] = on ? v[i] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[i];                 // frame order
+    }
+    if (e < nfix) c.sGAcc[e] += s;
+    else c.sGdV[(r0 + w) * kD + d] += s;
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane == 0) lds_store_flag(c.sGseq, f + 1);
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
@@ -882,8 +978,13 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
             prefetch(fi, t + 1, tgB);
           }
         }
-        frame_grad(a, lay, c, fb, pw + fi * NP);
+        frame_grad(a, lay, c, pw + fi * NP);
       }
+      // every producer done with the chunk's frames -> add the ring
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) atomicAdd(c.sGseq, 1);
+      poll_word(c.sGseq, NP * (fb / lay.fc + 1));
+      if (ntact > 0) grad_chunk_sum(a, c, fb, cnt, NP);   // (no active pedestrian: all zero)
     } else {
       for (int k = 0; k < nitems; k += 2) {
         item(k, tgA);
@@ -946,18 +1047,24 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     if (n0 < c.nact) {
       const float* prow = a.pos + (size_t)c.s * a.d.W * Nmax * 2;
       const int nks = (lay.wtot + 3) / 4;
-      #pragma unroll 1
-      for (int ks = 0; ks < nks; ++ks) {
-        const int w = 4 * ks + q;
-        float av = 0.f, bv = 0.f;
-        if (w < lay.wtot) {
-          if (n < c.nact) {
-            const float2 p = *reinterpret_cast<const float2*>(prow + ((size_t)w * Nmax + n) * 2);
-            av = __builtin_amdgcn_sqrtf(fmaf(p.x, p.x, p.y * p.y));
-          }
-          bv = c.sGdV[w * kD + L];
+      const int nc = n < c.nact ? n : 0;
+      // four k-steps' position loads in flight (clamped rows, selected after)
+#pragma unroll 1
+      for (int k0 = 0; k0 < nks; k0 += 4) {
+        float2 p[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int w = 4 * (k0 + i) + q;
+          p[i] = *reinterpret_cast<const float2*>(prow + ((size_t)(w < lay.wtot ? w : 0) * Nmax + nc) * 2);
         }
-        acc4 = mfma4(av, bv, acc4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int w = 4 * (k0 + i) + q;
+          const bool ok = k0 + i < nks && w < lay.wtot;
+          const float av = (ok && n < c.nact) ? __builtin_amdgcn_sqrtf(fmaf(p[i].x, p[i].x, p[i].y * p[i].y)) : 0.f;
+          const float bv = ok ? c.sGdV[(w < lay.wtot ? w : 0) * kD + L] : 0.f;
+          acc4 = mfma4(av, bv, acc4);
+        }
       }
     }
 #pragma unroll
@@ -1029,7 +1136,8 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.sMflag = reinterpret_cast<int*>(smem + lay.o_mflag);
   c.sY = smem + lay.o_y;
   c.sTicket = reinterpret_cast<int*>(c.sRed + 2 * kRB) + kRecW;
-  c.sCost = smem + lay.o_cost; c.sGFrame = smem + lay.o_gframe; c.sGAcc = smem + lay.o_gacc;
+  c.sCost = smem + lay.o_cost; c.sGFrame = smem + lay.o_gframe; c.sGRing = smem + lay.o_gring;
+  c.sGAcc = smem + lay.o_gacc;
   c.sGdV = smem + lay.o_gdv; c.sGdWo = smem + lay.o_gdwo;
   c.sGseq = reinterpret_cast<int*>(smem + lay.o_gseq);
   if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket

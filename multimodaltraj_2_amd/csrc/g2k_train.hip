@@ -8,26 +8,36 @@
 namespace g2k {
 namespace {
 
-// grad[p] = sum_s rows[s][p]: workgroup = 64 columns x 4 row slices; slice k
-// sums rows k, k + 4, ... in order, then the four slices in order (the same
-// sum for every launch: deterministic, no atomics)
-__global__ void __launch_bounds__(256) g2k_grad_rows_kernel(const float* __restrict__ rows, int S,
-                                                            int width, float* __restrict__ grad) {
-  __shared__ float red[4][64];
+// grad[p] = sum_s rows[s][p]: workgroup = 64 columns x 16 row slices; slice
+// k sums rows k, k + 16, ... in order (eight loads in flight), then the 16
+// slices in order (the same sum for every launch: deterministic, no atomics)
+constexpr int kRowSlices = 16;
+__global__ void __launch_bounds__(64 * kRowSlices) g2k_grad_rows_kernel(const float* __restrict__ rows,
+                                                                        int S, int width,
+                                                                        float* __restrict__ grad) {
+  __shared__ float red[kRowSlices][64];
   const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const int p = blockIdx.x * 64 + c;
-  float a0 = 0.f, a1 = 0.f;
+  float acc = 0.f;
   if (p < width) {
     int r = sl;
-    for (; r + 4 < S; r += 8) {           // two rows in flight per step
-      a0 += rows[(size_t)r * width + p];
-      a1 += rows[(size_t)(r + 4) * width + p];
+    for (; r + 7 * kRowSlices < S; r += 8 * kRowSlices) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = rows[(size_t)(r + i * kRowSlices) * width + p];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc += v[i];
     }
-    if (r < S) a0 += rows[(size_t)r * width + p];
+    for (; r < S; r += kRowSlices) acc += rows[(size_t)r * width + p];
   }
-  red[sl][c] = a0 + a1;
+  red[sl][c] = acc;
   __syncthreads();
-  if (sl == 0 && p < width) grad[p] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+  if (sl == 0 && p < width) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kRowSlices; ++k) t += red[k][c];
+    grad[p] = t;
+  }
 }
 
 // Optimizer step (argParser.py:38-47: grad_clip, learning_rate, decay_rate):
@@ -108,8 +118,8 @@ __global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ pa
 }  // namespace
 
 int grad_rows_launch(const float* rows, int S, int width, float* grad, hipStream_t st) {
-  hipLaunchKernelGGL(g2k_grad_rows_kernel, dim3((width + 63) / 64), dim3(256), 0, st, rows, S, width,
-                     grad);
+  hipLaunchKernelGGL(g2k_grad_rows_kernel, dim3((width + 63) / 64), dim3(64 * kRowSlices), 0, st, rows,
+                     S, width, grad);
   return check_launch("g2k_grad_rows_kernel");
 }
 

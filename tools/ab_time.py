@@ -1,0 +1,154 @@
+"""A/B timing of source variants of the scene kernel (development tool, not
+product code).  Each variant is a set of text replacements applied to a temp
+copy of multimodaltraj_2_amd/csrc; the copy is built into /tmp and timed on
+the bench workload (HIP events, reference-mode step and train step).
+
+usage: python tools/ab_time.py [CONFIG] [VARIANT ...]   (variants: see VARIANTS)"""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from multimodaltraj_2_amd import _lib, build, frame_step as fs, train_step as ts  # noqa: E402
+from multimodaltraj_2_amd.synthetic import CONFIGS, make_batch  # noqa: E402
+
+SCENE = "g2k_scene.hip"
+# diagnostic build: s_memtime stamps (low 32 bits) of scene 0's producer 0 /
+# recurrence wave 0 written past the gradient rows of a widened workspace
+STAMP_DEF = """
+#define G2K_ST(k, cond) do { if ((cond) && c.lane == 0 && a.grad_rows) { \\
+  const unsigned long long _t = __builtin_amdgcn_s_memtime(); \\
+  reinterpret_cast<unsigned*>(a.grad_rows)[(size_t)a.d.S * (24 * a.d.Nmax + 498) + (size_t)c.s * 64 + (k)] \\
+      = (unsigned)_t; } } while (0)
+"""
+P0 = "c.wv == kRecW"
+STAMPS = [
+    ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", STAMP_DEF + "namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk"),
+    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});",
+     "    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});\n    G2K_ST(1, " + P0 + " && fb == 0);"),
+    ("    // phase 2 — predictions and errors (GRAD: and the gradient)",
+     "    G2K_ST(2, " + P0 + " && fb == 0);\n    // phase 2 — predictions and errors (GRAD: and the gradient)"),
+    ("        frame_grad(a, lay, c, pw + fi * NP);",
+     "        G2K_ST(3 + fi, " + P0 + " && fb == 0 && fi < 5);\n        frame_grad(a, lay, c, pw + fi * NP);\n        G2K_ST(8 + fi, " + P0 + " && fb == 0 && fi < 4);"),
+    ("      poll_word(c.sGseq, NP * (fb / lay.fc + 1));",
+     "      G2K_ST(24 + pw, fb == 0);\n      poll_word(c.sGseq, NP * (fb / lay.fc + 1));\n      G2K_ST(12, " + P0 + " && fb == 0);"),
+    ("      if (ntact > 0) grad_chunk_sum(a, c, fb, cnt, NP);   // (no active pedestrian: all zero)",
+     "      if (ntact > 0) grad_chunk_sum(a, c, fb, cnt, NP);   // (no active pedestrian: all zero)\n      G2K_ST(13, " + P0 + " && fb == 0);"),
+    ("  ticket = __builtin_amdgcn_readfirstlane(ticket);", "  ticket = __builtin_amdgcn_readfirstlane(ticket);\n  G2K_ST(14, " + P0 + ");"),
+    ("  poll_word(c.sTicket, NP);", "  poll_word(c.sTicket, NP);\n  G2K_ST(15, " + P0 + ");"),
+    ("  // the small blocks and dWo, entry by entry", "  G2K_ST(16, " + P0 + ");\n  // the small blocks and dWo, entry by entry"),
+    ("  rc.store(a.h_out", "  G2K_ST(20, c.wv == 0);\n  rc.store(a.h_out"),
+    ("      const FrameHeadOut hd =", "      G2K_ST(30 + 3 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n      const FrameHeadOut hd ="),
+    ("      if (L < kL && q < 2) {\n        float* m = c.sMring", "      G2K_ST(31 + 3 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n      if (L < kL && q < 2) {\n        float* m = c.sMring"),
+    ("        lds_store_flag(c.sFlag + fl, f + 1);\n      }\n", "        lds_store_flag(c.sFlag + fl, f + 1);\n      }\n      G2K_ST(32 + 3 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n"),
+]
+NO_RECUR = [("  const bool live = a.h_in != nullptr;", "  const bool live = false;")]
+VARIANTS = {
+    "base": {},
+    "no_finalize": {SCENE: [("  poll_word(c.sTicket, NP);\n  const int P = 24 * Nmax + 496;",
+                             "  return;\n  poll_word(c.sTicket, NP);\n  const int P = 24 * Nmax + 496;")]},
+    "no_frame_grad": {SCENE: [("        frame_grad(a, lay, c, pw + fi * NP);", "")]},
+    "no_tile_grad": {SCENE: [("  if (GRAD) {\n    // the dY entries of other lanes",
+                              "  if (false) {\n    // the dY entries of other lanes")]},
+    "stamps": {SCENE: STAMPS},
+    "stamps_norecur": {SCENE: STAMPS + NO_RECUR},
+}
+
+
+def build_variant(name):
+    src = os.path.join(ROOT, "multimodaltraj_2_amd", "csrc")
+    tmp = tempfile.mkdtemp(prefix=f"g2k_{name}_")
+    for f in os.listdir(src):
+        shutil.copy(os.path.join(src, f), tmp)
+    for fname, reps in VARIANTS[name].items():
+        p = os.path.join(tmp, fname)
+        s = open(p).read()
+        for a, b in reps:
+            assert a in s, (name, a[:60])
+            s = s.replace(a, b)
+        open(p, "w").write(s)
+    out = f"/tmp/libg2k_{name}.so"
+    objs = []
+    for f in sorted(os.listdir(tmp)):
+        if f.endswith(".hip"):
+            o = os.path.join(tmp, f[:-4] + ".o")
+            subprocess.run([build.HIPCC, *build.FLAGS, "-c", "-o", o, os.path.join(tmp, f)],
+                           check=True)
+            objs.append(o)
+    subprocess.run([build.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs],
+                   check=True)
+    return out
+
+
+def time_it(fn, reps=200, warm=20):
+    for _ in range(warm):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def stamps(lib, c, t, dev):
+    """Run the stamps build once and print scene 0's timeline (cycles)."""
+    import ctypes
+    import numpy as np
+    params = fs.init_params(c["Nmax"], seed=0, device=dev)
+    tp = ts.TrainPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+    S, P2 = t["pos"].shape[0], ts.grad_size(c["Nmax"]) + 2
+    ws = torch.zeros(S * P2 * 4 + S * 64 * 4, dtype=torch.uint8, device=dev)
+    head = list(tp._head)
+    head[15], head[16] = ws.data_ptr(), ws.numel()
+    for _ in range(5):
+        rc = lib.g2k_train_step_f32(*head, None, None, 0.0, 0.0, 0.0, tp._stream)
+        assert rc == 0
+    torch.cuda.synchronize()
+    st = ws[S * P2 * 4:].view(torch.int32).reshape(S, 64).cpu().numpy().astype(np.int64)
+    for sc in (0, S // 2, S - 1):
+        r = st[sc]
+        rel = (r - r[0]) % (1 << 32)
+        names = {1: "B2", 2: "heads", 3: "tiles f0", 4: "tiles f1", 5: "tiles f2", 8: "fgrad f0",
+                 9: "fgrad f1", 10: "fgrad f2", 12: "chunk sync", 13: "chunk sum", 14: "ticket",
+                 15: "ticket=NP", 16: "dWi done", 20: "recur end"}
+        print(f"scene {sc} n_active {int(t['n_active'][sc])}: " +
+              "  ".join(f"{v}:{rel[k]}" for k, v in names.items() if r[k] != 0))
+        print("   producers' tiles done:", " ".join(str(rel[24 + p]) for p in range(8)))
+        print("   heads (start, head done, flags):", " ".join(f"({rel[30 + 3 * i]},{rel[31 + 3 * i]},{rel[32 + 3 * i]})" for i in range(3)))
+
+
+def main():
+    args = sys.argv[1:]
+    cfg = args[0] if args and args[0] in CONFIGS else "eth_hotel_synth"
+    names = [a for a in args if a in VARIANTS] or [v for v in VARIANTS if not v.startswith("stamps")]
+    c = dict(CONFIGS[cfg])
+    S = c["S"] if c["S"] <= 256 else c["S"] // 8
+    dev = torch.device("cuda")
+    b = make_batch(S, c["Nmax"], c["H"], seed=1)
+    t = b.to_device(dev)
+    for name in names:
+        lib = _lib.load(build_variant(name))
+        _lib._lib = lib
+        if name.startswith("stamps"):
+            stamps(lib, c, t, dev)
+            continue
+        params = fs.init_params(c["Nmax"], seed=0, device=dev)
+        plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+        tstep = ts.TrainStep(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
+                             t["h0"])
+        print(f"{cfg} {name:16s} fwd {time_it(plan.run):7.2f} us   train {time_it(tstep.run):7.2f} us",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
