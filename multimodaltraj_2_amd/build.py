@@ -20,18 +20,26 @@ OBJ = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fno-slp-vectorize", "-std=c++17", "-fPIC",
          "-I" + os.path.join(ROOT, "include")]
+# the scene kernel: no loop strength reduction (its per-stream induction
+# registers cost more VGPRs than the address arithmetic they save; measured
+# 125 -> 119 VGPRs, no spills in train mode's producers)
+FILE_FLAGS = {"g2k_scene.hip": ["-mllvm", "-disable-lsr"]}
+
+
+def flags_for(src):
+    return FLAGS + FILE_FLAGS.get(os.path.basename(src), [])
 
 
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in SRC + HDR)
+    return any(os.path.getmtime(p) > t for p in SRC + HDR + [os.path.abspath(__file__)])
 
 
 def _compile(src, verbose):
     obj = os.path.join(OBJ, os.path.basename(src)[:-4] + ".o")
-    cmd = [HIPCC, *FLAGS, "-c", "-o", obj, src]
+    cmd = [HIPCC, *flags_for(src), "-c", "-o", obj, src]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -274,20 +274,127 @@ def write_bundle(prefix: str, tensors: dict):
     return names
 
 
-def save_params(prefix: str, params, scope: str = "krnl_weights"):
-    """Checkpoint a G2KParams (torch tensors, any device) under TF-style names
-    (train.py:330-343 cadence; float32)."""
+# G2KParams field -> (variable scope, variable name) in the reference's graph:
+# weight_input/{weight_i, weight_ii} (train.py:167-175), krnl_weights/{weight_v,
+# bias_v, weight_o, weight_c} (models/g2k_lstm_mcr.py:38-69), krnl_embed/weight_r
+# (models/g2k_lstm_mcr.py:71-76).  TF uniquifies a scope opened again in the same
+# graph as <scope>_<k>; the reference opens them once per batch, so its
+# checkpoints hold krnl_weights_288/weight_v ... krnl_weights_307/weight_v.
+REF_NAMES = {
+    "Wi": ("weight_input", "weight_i"),
+    "Wii": ("weight_input", "weight_ii"),
+    "Wv": ("krnl_weights", "weight_v"),
+    "bv": ("krnl_weights", "bias_v"),
+    "Wo": ("krnl_weights", "weight_o"),
+    "Wc": ("krnl_weights", "weight_c"),
+    "Wr": ("krnl_embed", "weight_r"),
+}
+
+
+def _scope(scope: str, k: int) -> str:
+    return scope if k == 0 else f"{scope}_{k}"
+
+
+def ref_name(field: str, k: int = 0) -> str:
+    scope, var = REF_NAMES[field]
+    return f"{_scope(scope, k)}/{var}"
+
+
+def checkpoint_prefix(save_dir: str, d: int, e: int, b: int, num_batches: int) -> str:
+    """The reference's checkpoint path for dataset d, epoch e, batch b
+    (train.py:332-341: g2k_MPC_model_kfold_train_{d}_{e}_{b}.ckpt, saved with
+    global_step = e * num_batches + b)."""
+    return os.path.join(save_dir, f"g2k_MPC_model_kfold_train_{d}_{e}_{b}.ckpt-{e * num_batches + b}")
+
+
+def save_due(e: int, b: int, num_batches: int, save_every: int) -> bool:
+    """train.py:330: a checkpoint whenever (e * num_batches + b) % save_every == 0."""
+    return (e * num_batches + b) % save_every == 0
+
+
+def save_params(prefix: str, params, scope_index: int = 0, extras: dict | None = None,
+                dtype=np.float64):
+    """Checkpoint a G2KParams (torch tensors, any device) under the reference's
+    variable names (REF_NAMES; scopes suffixed _<scope_index> when > 0), in the
+    reference's dtype (float64: tf.float64 variables), then point the
+    directory's ``checkpoint`` state file at it (tf.train.Saver.save).
+    ``extras``: more {name: array} for the bundle (e.g. the last frame's
+    krnl_weights/cost).  Returns the names written."""
     from dataclasses import fields
-    t = {f"{scope}/{f.name}": getattr(params, f.name).detach().cpu().numpy() for f in fields(params)}
-    return write_bundle(prefix, t)
+    t = {ref_name(f.name, scope_index): getattr(params, f.name).detach().cpu().numpy().astype(dtype)
+         for f in fields(params)}
+    t.update(extras or {})
+    names = write_bundle(prefix, t)
+    write_state(os.path.dirname(os.path.abspath(prefix)), prefix)
+    return names
 
 
-def load_params(prefix: str, scope: str = "krnl_weights", device="cpu"):
-    """Inverse of save_params -> G2KParams on `device`."""
+def _scope_indices(names) -> list[int]:
+    out = set()
+    for n in names:
+        scope = n.split("/")[0]
+        if scope == "krnl_weights":
+            out.add(0)
+        elif scope.startswith("krnl_weights_") and scope[13:].isdigit():
+            out.add(int(scope[13:]))
+    return sorted(out)
+
+
+def load_params(prefix: str, scope_index: int | None = None, nmax: int | None = None,
+                device="cpu"):
+    """G2KParams (float32) from a bundle with the reference's variable names:
+    our own save_params output or a reference checkpoint.  ``scope_index``:
+    which <scope>_<k> instance (default: the last one, the reference's final
+    batch).  ``nmax``: pad the pedestrian axis (Wi rows, Wo columns) with
+    zeros to this width (the reference sizes them by the batch's num_nodes)."""
     import torch
 
     from .frame_step import G2KParams
     from dataclasses import fields
     t = read_bundle(prefix)
-    return G2KParams(**{f.name: torch.from_numpy(np.ascontiguousarray(
-        t[f"{scope}/{f.name}"], dtype=np.float32)).to(device) for f in fields(G2KParams)})
+    ks = _scope_indices(t)
+    if not ks:
+        raise KeyError(f"{prefix}: no krnl_weights scope")
+    k = ks[-1] if scope_index is None else scope_index
+    vals = {}
+    for f in fields(G2KParams):
+        name = ref_name(f.name, k)
+        if name not in t:
+            raise KeyError(f"{prefix}: {name} missing")
+        vals[f.name] = np.asarray(t[name], dtype=np.float32)
+    n = vals["Wi"].shape[0]
+    if nmax is not None and nmax > n:
+        vals["Wi"] = np.concatenate([vals["Wi"], np.zeros((nmax - n, vals["Wi"].shape[1]), np.float32)], 0)
+        vals["Wo"] = np.concatenate([vals["Wo"], np.zeros((vals["Wo"].shape[0], nmax - n), np.float32)], 1)
+    return G2KParams(**{kk: torch.from_numpy(np.ascontiguousarray(v)).to(device) for kk, v in vals.items()})
+
+
+def write_state(save_dir: str, prefix: str):
+    """The ``checkpoint`` state file tf.train.Saver.save writes next to the
+    bundles (a CheckpointState text proto; the reference's Saver is created per
+    save, so it lists the one path; train.py:383 reads it back)."""
+    path = os.path.abspath(prefix)
+    with open(os.path.join(save_dir, "checkpoint"), "w") as f:
+        f.write(f'model_checkpoint_path: "{path}"\nall_model_checkpoint_paths: "{path}"\n')
+
+
+def read_state(save_dir: str) -> str | None:
+    """tf.train.get_checkpoint_state(save_dir).model_checkpoint_path (train.py:
+    383): the latest prefix, relative paths taken from save_dir; None without a
+    state file."""
+    p = os.path.join(save_dir, "checkpoint")
+    if not os.path.exists(p):
+        return None
+    for line in open(p):
+        key, _, val = line.partition(":")
+        if key.strip() == "model_checkpoint_path":
+            path = val.strip().strip('"')
+            return path if os.path.isabs(path) else os.path.join(save_dir, path)
+    return None
+
+
+def epoch_of(prefix: str) -> int:
+    """The epoch in a checkpoint path, as train.py:387-389 parses it (the
+    second `_<digits>` group)."""
+    import re
+    return int(re.findall(r"_[0-9]+", prefix)[1].replace("_", ""))

@@ -45,6 +45,7 @@ constexpr int SM_K1 = 640;
 constexpr int SM_K2 = 752;
 constexpr int kSceneSmall = 1088;
 constexpr int kKA = 12;       // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
+constexpr int kYP = 17;       // train: per-producer dY tile scratch [24][kYP] (pitch: bank spread)
 // train mode
 constexpr int kGFrame = 384;  // per-producer frame scratch: dM [24][8], dcost [8][8], dE [8][16]
 constexpr int kGT_DM = 0, kGT_DC = 192, kGT_DE = 256;
@@ -76,7 +77,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
-  s.o_y = o;     o += NP * kD * kL2;                  // tile transpose scratch (Y, then dY)
+  s.o_y = o;     o += grad ? NP * kL2 * kYP : 0;      // dY tile scratch (train)
   s.o_met = o;   o += NP * 8;
   s.o_ring = o;  o += fc * kD * kD;
   s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
@@ -535,87 +536,101 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
            c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);
 }
 
-// One 16-pedestrian tile of one frame: Y^T = Wo^T @ M^T (M = this frame's
-// [24][8] from the M ring; models/g2k_lstm_mcr.py:122-124), pred stores
-// (active columns only, in groups of four), the a9 error terms (train.py:
-// 640-656; four lanes per pedestrian, three prediction steps each).
-// GRAD: dY = (Y - target) on active, masked pedestrians replaces Y in the
-// tile scratch, its squares go to lsum, and the tile's products are formed:
-//   dM   += dY @ Wo^T   (added into the frame's dM [24][8] in LDS)
-//   dWoT  = dY^T @ M    (lane (L, q) reg v: dWo[t = L][n0 + 4q + v])
+// LDS hand-off between the lanes of ONE wave: DS instructions of a wave
+// complete in issue order, so only compiler reordering has to be fenced
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One 16-pedestrian tile of one frame (models/g2k_lstm_mcr.py:122-124):
+// Y = M @ Wo with M = this frame's [24][8] from the M ring.  The rows are
+// taken in the targets' interleaved order r = 2 step + xy (physical M / pred
+// row mrow(r)), so lane (L, q) ends with Y[r][n0 + L] for r = 4q + v (block
+// 0) and r = 16 + 4q + v (block 1, q < 2): pedestrian n0 + L, steps 2q, 2q+1
+// and 8+2q, 9+2q, exactly the two float4s of its target row it loaded (tg).
+// The a9 error terms (train.py:640-656) are per-lane sums over those steps,
+// then across the four lane groups (permlane swaps); no LDS transpose.
+// pred stores: active columns only (n < n_active), one 64-B row segment per
+// lane group and row.
+// GRAD: dY = (Y - target) on active, masked pedestrians, its squares into
+// lsum, and the tile's products:
+//   dWoT  = dY^T @ M     (from the registers; lane (L, q) reg v: dWo[t = L][n0 + 4q + v])
+//   dm   += dY @ Wo^T    (dY through the wave's [24][17] scratch; dm[0][v] =
+//                         dM[r = 4q + v][t = L], dm[1][v] = dM[r = 16 + 4q + v][t = L],
+//                         accumulated over the frame's tiles in registers)
+__device__ __forceinline__ int mrow(int r) { return (r & 1) * kL + (r >> 1); }
+
 template <bool GRAD>
 __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, float* pr,
-                                          const float2 (&tg)[3], const uint8_t* pm, int Nmax,
-                                          int nact, int t, int L, int q, int lane, float acc[5],
-                                          float& lsum, float* dM, f32x4& dWoT) {
-  const int pp = lane >> 2, u = lane & 3;
-  const int n0 = 16 * t;
-  const int ne = n0 + pp;
-  const bool has_t = ne < nact && (pm ? pm[ne] != 0 : true);
+                                          const float2 (&tg)[4], bool has_t, int Nmax, int nact,
+                                          int t, int L, int q, float acc[5], float& lsum,
+                                          f32x4 (&dm)[2], f32x4& dWoT) {
+  const int n0 = 16 * t, n = n0 + L;
+  const bool hi = q < 2;                                   // block-1 rows exist (r < 24)
   f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
+  float bm[8];                                             // GRAD: M[r][t = L & 7], r as in dWoT
   {
     // unconditional loads at clamped addresses, selects after (see frame_head)
-    const int n = n0 + L, nc = n < Nmax ? n : Nmax - 1, Lx = L < kL ? L : 0;
-    float wo[2], bx[2], by[2];
+    const int nc = n < Nmax ? n : Nmax - 1, L7 = L & 7;
+    float a0[2], a1[2], wo[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int k = 4 * ks + q;
-      wo[ks] = sWo[k * Nmax + nc];
-      bx[ks] = M[Lx * kT + k];
-      by[ks] = M[(kL + Lx) * kT + k];
+      a0[ks] = M[mrow(L) * kT + k];                        // A[r = L][k]
+      a1[ks] = M[mrow(16 + L7) * kT + k];                  // A[r = 16 + L][k]
+      wo[ks] = sWo[k * Nmax + nc];                         // B[k][n = n0 + L]
     }
-    asm volatile("" : "+v"(wo[0]), "+v"(wo[1]), "+v"(bx[0]), "+v"(bx[1]), "+v"(by[0]), "+v"(by[1]));
+    if (GRAD) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bm[ks] = M[mrow(4 * q + ks) * kT + L7];
+        bm[4 + ks] = M[mrow(16 + 4 * (q & 1) + ks) * kT + L7];
+      }
+      asm volatile("" : "+v"(bm[0]), "+v"(bm[1]), "+v"(bm[2]), "+v"(bm[3]), "+v"(bm[4]), "+v"(bm[5]),
+                   "+v"(bm[6]), "+v"(bm[7]));
+    }
+    asm volatile("" : "+v"(a0[0]), "+v"(a0[1]), "+v"(a1[0]), "+v"(a1[1]), "+v"(wo[0]), "+v"(wo[1]));
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const float w = n < nact ? wo[ks] : 0.f;
-      y0 = mfma4(w, L < kL ? bx[ks] : 0.f, y0);   // Y[L][n0 + 4q + i]
-      y1 = mfma4(w, L < kL ? by[ks] : 0.f, y1);   // Y[12 + L][n0 + 4q + i]
+      y0 = mfma4(a0[ks], w, y0);                           // Y[4q + v][n]
+      y1 = mfma4(L < kT ? a1[ks] : 0.f, w, y1);            // Y[16 + 4q + v][n] (0 for q >= 2)
     }
   }
-  if (L < kL) {
-    const int nb = n0 + 4 * q;
-    if (pr && nb < nact) {    // padded columns (n >= n_active) are left untouched
-      if (nb + 3 < Nmax && ((Nmax & 3) == 0)) {
-        *reinterpret_cast<float4*>(pr + L * Nmax + nb) = make_float4(y0[0], y0[1], y0[2], y0[3]);
-        *reinterpret_cast<float4*>(pr + (kL + L) * Nmax + nb) = make_float4(y1[0], y1[1], y1[2], y1[3]);
-      } else {
+  if (pr && n < nact) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (nb + i < Nmax) { pr[L * Nmax + nb + i] = y0[i]; pr[(kL + L) * Nmax + nb + i] = y1[i]; }
-      }
+    for (int v = 0; v < 4; ++v) {
+      pr[mrow(4 * q + v) * Nmax + n] = y0[v];
+      if (hi) pr[mrow(16 + 4 * q + v) * Nmax + n] = y1[v];
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<float2*>(ys + (4 * q + i) * kL2 + 2 * L) = make_float2(y0[i], y1[i]);
   }
-  __builtin_amdgcn_wave_barrier();
-  float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f, fx = 0.f, fy = 0.f;
-  float2* yp = reinterpret_cast<float2*>(ys + pp * kL2) + 3 * u;
-  float2 dyv[3];
+  // errors: d = Y - target, (x, y) pairs in registers (v = 0, 1 and 2, 3)
+  float d0[4], d1[4];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const float2 yv = yp[k];
-    const float dx = yv.x - tg[k].x, dy = yv.y - tg[k].y;
-    ea = fmaf(dx, dx, ea);
-    eb = fmaf(dx, dy, eb);
-    ec = fmaf(dy, dy, ec);
-    el2 += __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
-    fx = dx; fy = dy;
-    dyv[k] = make_float2(has_t ? dx : 0.f, has_t ? dy : 0.f);
+  for (int v = 0; v < 2; ++v) {
+    d0[2 * v] = y0[2 * v] - tg[v].x;       d0[2 * v + 1] = y0[2 * v + 1] - tg[v].y;
+    d1[2 * v] = hi ? y1[2 * v] - tg[2 + v].x : 0.f;
+    d1[2 * v + 1] = hi ? y1[2 * v + 1] - tg[2 + v].y : 0.f;
   }
-  if (GRAD) {
-    lsum += has_t ? ea + ec : 0.f;           // this lane's three steps
+  float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) yp[k] = dyv[k];   // dY over Y, in place (own entries only)
+  for (int h = 0; h < 2; ++h) {
+    const float* d = h ? d1 : d0;
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const float dx = d[2 * v], dy = d[2 * v + 1];
+      ea = fmaf(dx, dx, ea);
+      eb = fmaf(dx, dy, eb);
+      ec = fmaf(dy, dy, ec);
+      el2 += __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
+    }
   }
-  __builtin_amdgcn_wave_barrier();
-  ea += dpp<0xB1>(ea); ea += dpp<0x4E>(ea);
-  eb += dpp<0xB1>(eb); eb += dpp<0x4E>(eb);
-  ec += dpp<0xB1>(ec); ec += dpp<0x4E>(ec);
-  el2 += dpp<0xB1>(el2); el2 += dpp<0x4E>(el2);
-  fx = dpp<0xFF>(fx);   // quad_perm [3,3,3,3]: the fde vector lives in quarter 3
-  fy = dpp<0xFF>(fy);
-  if (has_t && u == 0) {
+  ea += partner16(ea); eb += partner16(eb); ec += partner16(ec); el2 += partner16(el2);
+  ea += partner32(ea); eb += partner32(eb); ec += partner32(ec); el2 += partner32(el2);
+  if (has_t && q == 1) {                   // group 1 holds the last step (r = 22, 23)
+    const float fx = d1[2], fy = d1[3];
     const float hm = 0.5f * (ea - ec);
     const float lam = 0.5f * (ea + ec) + __builtin_amdgcn_sqrtf(fmaf(hm, hm, eb * eb));
     const float fsq = fmaf(fx, fx, fy * fy);
@@ -624,77 +639,52 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
     acc[2] += fsq;
     acc[3] += el2 * (1.0f / 12.0f);
     acc[4] += __builtin_amdgcn_sqrtf(fsq);
+    if (GRAD) lsum += ea + ec;
   }
   if (GRAD) {
-    // the dY entries of other lanes: LDS in order within the wave, so only
-    // the compiler has to be kept from moving the reads above the writes
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // dM += dY @ Wo^T: A[r = L][k] = dY[r][n0 + k], B[k][t = L] = Wo[t][n0 + k], k = 4q + ks
-    {
-      float ax[4], ay[4], bw[4];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int k = 4 * q + ks;
-        const float2 d = *reinterpret_cast<const float2*>(ys + k * kL2 + 2 * (L < kL ? L : 0));
-        ax[ks] = d.x;
-        ay[ks] = d.y;
-        const int n = n0 + k;
-        bw[ks] = sWo[(L & 7) * Nmax + (n < Nmax ? n : 0)];
-      }
-      asm volatile("" : "+v"(ax[0]), "+v"(ax[1]), "+v"(ax[2]), "+v"(ax[3]), "+v"(ay[0]), "+v"(ay[1]),
-                   "+v"(ay[2]), "+v"(ay[3]), "+v"(bw[0]), "+v"(bw[1]), "+v"(bw[2]), "+v"(bw[3]));
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int n = n0 + 4 * q + ks;
-        ax[ks] = L < kL ? ax[ks] : 0.f;
-        ay[ks] = L < kL ? ay[ks] : 0.f;
-        bw[ks] = (L < kT && n < nact) ? bw[ks] : 0.f;
-      }
-      f32x4 mx = {0.f, 0.f, 0.f, 0.f}, my = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        mx = mfma4(ax[ks], bw[ks], mx);
-        my = mfma4(ay[ks], bw[ks], my);
-      }
-      // into the frame's dM [24][8] (this wave's scratch), tile after tile
-      if (L < kT && q < 3) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          dM[(4 * q + v) * kT + L] += mx[v];
-          dM[(kL + 4 * q + v) * kT + L] += my[v];
-        }
-      }
+    for (int v = 0; v < 4; ++v) {
+      d0[v] = has_t ? d0[v] : 0.f;
+      d1[v] = has_t ? d1[v] : 0.f;
     }
-    // dWo^T = dY^T @ M: A[n = L][r] = dY[r][n0 + L], B[r][t = L] = M[r][t], r = 4 ks + q
+    // dY into the scratch [r][n] (pitch kYP) for dM, where n must be the
+    // contraction index
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      ys[(4 * q + v) * kYP + L] = d0[v];
+      if (hi) ys[(16 + 4 * q + v) * kYP + L] = d1[v];
+    }
+    // dWo^T = dY^T @ M: A[n = L][r] = dY[r][n0 + L] (registers), B[r][t = L] = M[r][t]
     {
-      float ar[6], br[6];
-#pragma unroll
-      for (int ks = 0; ks < 6; ++ks) {
-        const int r = 4 * ks + q;
-        const int col = r < kL ? 2 * r : 2 * (r - kL) + 1;
-        ar[ks] = ys[L * kL2 + col];
-        br[ks] = M[r * kT + (L & 7)];
-      }
-      asm volatile("" : "+v"(ar[0]), "+v"(ar[1]), "+v"(ar[2]), "+v"(ar[3]), "+v"(ar[4]), "+v"(ar[5]),
-                   "+v"(br[0]), "+v"(br[1]), "+v"(br[2]), "+v"(br[3]), "+v"(br[4]), "+v"(br[5]));
-#pragma unroll
-      for (int ks = 0; ks < 6; ++ks) br[ks] = L < kT ? br[ks] : 0.f;
       f32x4 w = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 6; ++ks) w = mfma4(ar[ks], br[ks], w);
+      for (int ks = 0; ks < 4; ++ks) w = mfma4(d0[ks], bm[ks], w);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) w = mfma4(d1[ks], hi ? bm[4 + ks] : 0.f, w);
       dWoT = w;
     }
+    wave_lds_sync();
+    // dm += dY @ Wo^T: A[r = L][n] = dY[r][n0 + n] (scratch), B[n][t = L] = Wo[t][n0 + n]
+    {
+      float a0[4], a1[4], bw[4];
+      const int L7 = L & 7;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k = 4 * ks + q, nk = n0 + k;
+        a0[ks] = ys[L * kYP + k];
+        a1[ks] = ys[(16 + L7) * kYP + k];
+        bw[ks] = sWo[L7 * Nmax + (nk < Nmax ? nk : Nmax - 1)];
+      }
+      asm volatile("" : "+v"(a0[0]), "+v"(a0[1]), "+v"(a0[2]), "+v"(a0[3]), "+v"(a1[0]), "+v"(a1[1]),
+                   "+v"(a1[2]), "+v"(a1[3]), "+v"(bw[0]), "+v"(bw[1]), "+v"(bw[2]), "+v"(bw[3]));
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        dm[0] = mfma4(a0[ks], bw[ks], dm[0]);
+        dm[1] = mfma4(L < kT ? a1[ks] : 0.f, bw[ks], dm[1]);
+      }
+    }
+    wave_lds_sync();                       // scratch reads done before the next tile's writes
   }
-}
-
-// LDS hand-off between the lanes of ONE wave: DS instructions of a wave
-// complete in issue order, so only compiler reordering has to be fenced
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Wait (one LDS word, wave-uniform) until *w == want.
@@ -797,8 +787,7 @@ __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout&
       if (j < 11) tm[kL2 * kT + kT * 10 + j * kD + L] = d[v];
     }
   }
-  wave_lds_sync();
-  for (int o = lane; o < kL2 * kT; o += 64) dM[o] = 0.f;  // for this wave's next frame
+  wave_lds_sync();                                        // before the next frame's dM
 }
 
 // GRAD, once every producer is done with chunk [fb, fb + cnt): the ring's
@@ -849,12 +838,30 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
   const int pw = c.wv - kRecW, L = c.L, q = c.q, lane = c.lane, s = c.s, ntact = c.ntact;
-  const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
+  // pedestrian n = 16 t + L has targets (n < n_active and its
+  // ped_mask byte set): bit t of this lane's act_bits.  Read once, before the
+  // first staging wait (a mask load inside the tile loop would make the
+  // compiler wait for the targets prefetched behind it)
+  unsigned act_bits = 0;
+  {
+    const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
+    bool on[kMaxN / 64];
+#pragma unroll
+    for (int j = 0; j < kMaxN / 64; ++j) {
+      const int n = lane + 64 * j;
+      on[j] = n < c.nact && (pm ? pm[n < Nmax ? n : 0] != 0 : true);
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxN / 64; ++j) {
+      const unsigned long long b = __builtin_amdgcn_ballot_w64(on[j]);
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) act_bits |= (unsigned)((b >> (16 * tt + L)) & 1ull) << (4 * j + tt);
+    }
+  }
   // tile items of a chunk.  Forward: item j -> frame j / ntact, tile
   // j % ntact; this producer takes items pw, pw + NP, ...  GRAD: this
   // producer owns whole frames pw, pw + NP, ... (its k-th item is tile
   // k % ntact of its (k / ntact)-th frame)
-  const int pp = lane >> 2, u = lane & 3;
   auto item_ft = [&](int k, int& fl, int& t) {
     if (GRAD) {
       fl = pw + (k / ntact) * NP;
@@ -865,23 +872,24 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       t = j - fl * ntact;
     }
   };
-  float2 tgA[3] = {}, tgB[3] = {};
-  auto load_item = [&](int fb, int nitems, int k, float2 (&tg)[3]) {
+  // the tile's targets in pred_tile's order: pedestrian 16 t + L, floats
+  // 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row (zero for q >= 2)
+  float2 tgA[4] = {}, tgB[4] = {};
+  auto load_item = [&](int fb, int nitems, int k, float2 (&tg)[4]) {
     if (k >= nitems) return;
     int fl, t;
     item_ft(k, fl, t);
-    const int ne = 16 * t + pp;
+    const int ne = 16 * t + L;
     const int nc = ne < Nmax ? ne : 0;
     const float2* tp = reinterpret_cast<const float2*>(
-        a.targets + (((size_t)s * F + fb + fl) * Nmax + nc) * kL2) + 3 * u;
-    tg[0] = tp[0]; tg[1] = tp[1]; tg[2] = tp[2];
+        a.targets + (((size_t)s * F + fb + fl) * Nmax + nc) * kL2);
+    tg[0] = tp[2 * q]; tg[1] = tp[2 * q + 1];
+    tg[2] = tp[8 + 2 * (q & 1)]; tg[3] = tp[9 + 2 * (q & 1)];
+    if (q >= 2) tg[2] = tg[3] = make_float2(0.f, 0.f);
   };
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float lsum = 0.f;
-  if (GRAD) {                                          // this wave's dM starts at zero
-    float* dM0 = c.sGFrame + pw * kGFrame + kGT_DM;
-    for (int o = lane; o < kL2 * kT; o += 64) dM0[o] = 0.f;
-  }
+  f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // GRAD: the frame's dM (pred_tile)
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
@@ -930,17 +938,16 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       __builtin_amdgcn_s_setprio(0);
     }
     // phase 2 — predictions and errors (GRAD: and the gradient)
-    float* ys = c.sY + pw * kD * kL2;
-    float* dMs = GRAD ? c.sGFrame + pw * kGFrame + kGT_DM : nullptr;
-    auto item = [&](int k, const float2 (&tg)[3]) {
+    float* ys = c.sY + pw * kL2 * kYP;
+    auto item = [&](int k, const float2 (&tg)[4]) {
       int fl, t;
       item_ft(k, fl, t);
       const int f = fb + fl;
       poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)
       float* pr = a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : nullptr;
       f32x4 dWoT;
-      pred_tile<GRAD>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, pm, Nmax, c.nact, t, L, q, lane,
-                      acc, lsum, dMs, dWoT);
+      pred_tile<GRAD>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
+                      c.nact, t, L, q, acc, lsum, dm, dWoT);
       if (GRAD) {
         // dWo^T[n0 + 4q + v][t = L]: one copy per producer, or one copy
         // added to in frame order (tile sequence word) when that is too big
@@ -964,7 +971,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       // frame, else tile 0 (A) / 1 (B) of this producer's next frame — and
       // the frame's weight-side terms after its last tile (one call site)
       const int nfr = nitems / (ntact > 0 ? ntact : 1);
-      auto prefetch = [&](int fi, int t, float2 (&tg)[3]) {
+      auto prefetch = [&](int fi, int t, float2 (&tg)[4]) {
         const int tn = t + 2 < ntact ? t + 2 : (t & 1);
         const int fn = t + 2 < ntact ? fi : fi + 1;
         if (fn < nfr && tn < ntact) load_item(fb, nitems, fn * ntact + tn, tg);
@@ -978,6 +985,17 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
             prefetch(fi, t + 1, tgB);
           }
         }
+        // the frame's dM to this wave's scratch (M's physical rows), then its terms
+        if (L < kT) {
+          float* dMs = c.sGFrame + pw * kGFrame + kGT_DM;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            dMs[mrow(4 * q + v) * kT + L] = dm[0][v];
+            if (q < 2) dMs[mrow(16 + 4 * q + v) * kT + L] = dm[1][v];
+          }
+        }
+        dm[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dm[1] = f32x4{0.f, 0.f, 0.f, 0.f};
         frame_grad(a, lay, c, pw + fi * NP);
       }
       // every producer done with the chunk's frames -> add the ring

@@ -222,23 +222,25 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
 def mcr_forward(params: G2KParams, X, Rel, G, n_active, *, lam=LAMBDA, stream=None):
     """g2k_lstm_mcr.forward() for S feeds (models/g2k_lstm_mcr.py:99-124).
     X [S, D+2, D], Rel [S, 2, D], G [S, D, T] -> (attn [S,D,D], cost [S,T,T],
-    pred [S, 2L, Nmax])."""
+    pred [S, 2L, Nmax]); D = X.shape[2] in 1..16 (sample.py runs D = 10,
+    the reference checkpoints hold D = 10 weights)."""
     lib = _lib.load()
     dev = X.device
     S = int(X.shape[0])
+    D = int(X.shape[2]) if X.dim() == 3 else -1
     Nmax = int(params.Wo.shape[1])
-    for k, t, shp in (("X", X, (S, HIDDEN_LEN + 2, HIDDEN_LEN)), ("Rel", Rel, (S, 2, HIDDEN_LEN)),
-                      ("G", G, (S, HIDDEN_LEN, OBS_LEN))):
+    for k, t, shp in (("X", X, (S, D + 2, D)), ("Rel", Rel, (S, 2, D)), ("G", G, (S, D, OBS_LEN)),
+                      ("Wv", params.Wv, (OBS_LEN, D + 2)), ("bv", params.bv, (D,))):
         if tuple(t.shape) != shp:
             raise ValueError(f"{k}: shape {tuple(t.shape)}, expected {shp}")
         _check_dev(k, t, dev, torch.float32)
     _check_dev("n_active", n_active, dev, torch.int32)
-    for k in ("Wv", "bv", "Wr", "Wc", "Wo"):
+    for k in ("Wr", "Wc", "Wo"):
         _check_dev(k, getattr(params, k), dev, torch.float32)
-    attn = torch.empty((S, HIDDEN_LEN, HIDDEN_LEN), device=dev, dtype=torch.float32)
+    attn = torch.empty((S, D, D), device=dev, dtype=torch.float32)
     cost = torch.empty((S, OBS_LEN, OBS_LEN), device=dev, dtype=torch.float32)
     pred = torch.empty((S, 2 * PRED_LEN, Nmax), device=dev, dtype=torch.float32)
-    d = _lib.G2KDims(S, 1, OBS_LEN, PRED_LEN, HIDDEN_LEN, 64, Nmax, OBS_LEN, 0)
+    d = _lib.G2KDims(S, 1, OBS_LEN, PRED_LEN, D, 64, Nmax, OBS_LEN, 0)
     w = _lib.G2KWeights(None, None, params.Wv.data_ptr(), params.bv.data_ptr(),
                         params.Wr.data_ptr(), params.Wc.data_ptr(), params.Wo.data_ptr())
     rc = lib.g2k_mcr_forward_f32(ctypes.byref(d), ctypes.byref(w), _ptr(X), _ptr(Rel), _ptr(G),
@@ -250,15 +252,16 @@ def mcr_forward(params: G2KParams, X, Rel, G, n_active, *, lam=LAMBDA, stream=No
 
 def frame_recurrence(A, h, *, stream=None):
     """train.py:240-252 over F attention matrices: A [S, F, D, D], h [S, D, H]
-    (updated in place and returned)."""
+    (updated in place and returned); D in 1..16."""
     lib = _lib.load()
     S, F = int(A.shape[0]), int(A.shape[1])
     H = int(h.shape[2])
+    D = int(h.shape[1])
     _check_dev("A", A, A.device, torch.float32)
     _check_dev("h", h, A.device, torch.float32)
-    if tuple(A.shape[2:]) != (HIDDEN_LEN, HIDDEN_LEN) or tuple(h.shape) != (S, HIDDEN_LEN, H):
-        raise ValueError("A must be [S, F, 16, 16] and h [S, 16, H]")
-    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, 1, OBS_LEN, 0)
+    if tuple(A.shape[2:]) != (D, D) or tuple(h.shape) != (S, D, H):
+        raise ValueError(f"A must be [S, F, D, D] and h [S, D, H] (got {tuple(A.shape)}, {tuple(h.shape)})")
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, D, H, 1, OBS_LEN, 0)
     rc = lib.g2k_frame_recurrence_f32(ctypes.byref(d), _ptr(A), _ptr(h), F, _stream(stream))
     _lib.check("g2k_frame_recurrence_f32", rc)
     return h

@@ -7,8 +7,10 @@ TF feed/fetch becomes attribute assignment: set ``outputs``, ``ngh``,
 Build decisions: Q1 the fetched prediction is the
 dataflow result, never the random feed; Q2 fed tensors are used (not the
 placeholder defaults); Q6 parameters are plain seeded N(0,1) tensors (the
-``krnl_weights_21/*`` graph lookups are unavailable); ``sess_g`` is accepted
-and ignored.  D = in_features.shape[0] must be 16 (the HIP geometry).
+``krnl_weights_21/*`` graph lookups are unavailable — restore trained ones
+with ``weights=checkpoint_weights(prefix)``); ``sess_g`` is accepted and
+ignored.  D = in_features.shape[0] in 1..16 (train.py's 16, sample.py's
+num_freq_blocks = 10 and the reference checkpoints' 10).
 """
 from __future__ import annotations
 
@@ -29,9 +31,10 @@ class g2k_lstm_mcr:
     def __init__(self, in_features, hidden_size, obs_len, num_nodes, lambda_reg, sess_g=None,
                  *, device="cuda", seed=0, weights=None):
         D = _dim0(in_features)
-        if D != fs.HIDDEN_LEN or obs_len != fs.OBS_LEN:
-            raise ValueError(f"HIP g2k_lstm_mcr needs in_features.shape[0] == 16 and obs_len == 8 "
+        if not 1 <= D <= fs.HIDDEN_LEN or obs_len != fs.OBS_LEN:
+            raise ValueError(f"HIP g2k_lstm_mcr needs 1 <= in_features.shape[0] <= 16 and obs_len == 8 "
                              f"(got {D}, {obs_len})")
+        self.D = D
         self.device = torch.device(device)
         self.out_size = int(num_nodes)
         self.lambda_reg = float(lambda_reg)
@@ -75,14 +78,15 @@ class g2k_lstm_mcr:
         if self.weight_o.shape[1] < n:
             raise ValueError(f"weight_o has {self.weight_o.shape[1]} columns < out_size {n}")
         nmax = max(int(self.weight_o.shape[1]), 1)
-        params = fs.G2KParams(Wi=torch.zeros((nmax, 16), device=self.device),
-                              Wii=torch.zeros((16, 8), device=self.device),
+        D = self.D
+        params = fs.G2KParams(Wi=torch.zeros((nmax, D), device=self.device),
+                              Wii=torch.zeros((D, 8), device=self.device),
                               Wv=self.weight_v.contiguous(), bv=self.bias_v.contiguous(),
                               Wr=self.weight_r.contiguous(), Wc=self.weight_c.contiguous(),
                               Wo=self.weight_o.contiguous())
-        X = self.outputs.reshape(1, 18, 16).contiguous()
-        Rel = self.rel_features.reshape(1, 2, 16).contiguous()
-        G = self.ngh.reshape(1, 16, 8).contiguous()
+        X = self.outputs.reshape(1, D + 2, D).contiguous()
+        Rel = self.rel_features.reshape(1, 2, D).contiguous()
+        G = self.ngh.reshape(1, D, 8).contiguous()
         nact = torch.tensor([n], dtype=torch.int32, device=self.device)
         attn, cost, pred = fs.mcr_forward(params, X, Rel, G, nact, lam=self.lambda_reg)
         self.ngh_scaled = self.lambda_reg * self.ngh
@@ -91,3 +95,14 @@ class g2k_lstm_mcr:
         self.temp_path = pred[0, :, :n]
         self.pred_path_band = self.temp_path.reshape(2, fs.PRED_LEN, n)
         return self.pred_path_band
+
+
+def checkpoint_weights(prefix, scope_index=None, num_nodes=None, device="cuda"):
+    """The g2k_lstm_mcr variables of a TF checkpoint (checkpoint.load_params:
+    krnl_weights_<k>/{weight_v, bias_v, weight_o, weight_c}, krnl_embed_<k>/
+    weight_r; sample.py:213-225 restores them with tf.train.Saver) as the
+    ``weights=`` dict of g2k_lstm_mcr; weight_o padded with zero columns to
+    ``num_nodes``."""
+    from .. import checkpoint
+    p = checkpoint.load_params(prefix, scope_index=scope_index, nmax=num_nodes, device=device)
+    return dict(weight_v=p.Wv, bias_v=p.bv, weight_o=p.Wo, weight_c=p.Wc, weight_r=p.Wr)

@@ -10,8 +10,9 @@ loop as one fused HIP step (hidden state carried from batch to batch when
 ADE / FDE rows ``epoch,batch,ADE,FDE,num_peds`` to
 <log_dir>/g2k_MPC_error_log_kfold_<d>.csv.  The model weights are one seeded
 N(0, 1) draw (quirk Q15: the reference re-draws them every batch).  With
---save_dir they are written as TF tensor bundles every --save_every batches
-(train.py:330-343; multimodaltraj_2_amd/checkpoint.py).
+--save_dir they are written as TF tensor bundles under the reference's
+variable names and file names, with its global-step cadence and ``checkpoint``
+state file (train.py:330-343; multimodaltraj_2_amd/checkpoint.py).
 """
 from __future__ import annotations
 
@@ -64,9 +65,9 @@ def run_dataset(args, d, params_cache, device, log):
                 h = out.h
             ade, fde = fs.batch_errors(out.metrics, leave_dataset=args.leaveDataset, num_nodes=[n])
             rows.append((e, b, float(ade[0]), float(fde[0]), n))
-            if args.save_dir and b % args.save_every == 0:   # train.py:330-343 cadence
-                checkpoint.save_params(os.path.join(args.save_dir, f"g2k_mcr_model_{d}.ckpt-{e}"),
-                                       params_cache[key])
+            if args.save_dir and checkpoint.save_due(e, b, loader.num_batches, args.save_every):
+                checkpoint.save_params(checkpoint.checkpoint_prefix(args.save_dir, d, e, b, loader.num_batches),
+                                       params_cache[key])     # train.py:330-341
         log(f"dataset {d} epoch {e}: {len(rows)} batches, {time.time() - t0:.2f}s")
     return rows
 

@@ -49,13 +49,59 @@ def test_reencode_all_reference_checkpoints(tmp_path):
         _same_bytes(prefix, out)
 
 
-def test_params_roundtrip(tmp_path):
+MCRATTN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ckpt_mcrattn_289")
+
+
+def test_params_roundtrip_reference_names(tmp_path):
+    """save_params writes the reference's variable names (float64, as the
+    reference's tf.float64 variables), the reference's file name and the
+    `checkpoint` state file; load_params reads it back exactly."""
     p = fs.init_params(12, seed=3)
-    prefix = str(tmp_path / "save" / "g2k_model.ckpt-50")
+    save = tmp_path / "save"
+    prefix = ck.checkpoint_prefix(str(save), d=4, e=2, b=7, num_batches=30)
+    assert os.path.basename(prefix) == "g2k_MPC_model_kfold_train_4_2_7.ckpt-67"
     names = ck.save_params(prefix, p)
     assert names == sorted(names)
-    q = ck.load_params(prefix)
+    assert set(names) == {"weight_input/weight_i", "weight_input/weight_ii", "krnl_weights/weight_v",
+                          "krnl_weights/bias_v", "krnl_weights/weight_o", "krnl_weights/weight_c",
+                          "krnl_embed/weight_r"}
+    t = ck.read_bundle(prefix)
+    assert t["krnl_weights/weight_o"].dtype == np.float64 and t["krnl_weights/weight_o"].shape == (8, 12)
+    q = ck.load_params(ck.read_state(str(save)))
     for k in ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo"):
         assert torch.equal(getattr(p, k), getattr(q, k))
-    t = ck.read_bundle(prefix)
-    assert t["krnl_weights/Wo"].dtype == np.float32 and t["krnl_weights/Wo"].shape == (8, 12)
+    state = open(save / "checkpoint").read()
+    assert state == f'model_checkpoint_path: "{os.path.abspath(prefix)}"\n' \
+                    f'all_model_checkpoint_paths: "{os.path.abspath(prefix)}"\n'
+    assert ck.epoch_of(prefix) == 2                           # train.py:387-389
+    # a scoped copy (the reference's krnl_weights_<k>) and its selection
+    ck.save_params(str(save / "scoped.ckpt-1"), p, scope_index=21)
+    assert "krnl_weights_21/weight_v" in ck.read_bundle(str(save / "scoped.ckpt-1"))
+    assert ck.read_state(str(save)).endswith("scoped.ckpt-1")
+    q = ck.load_params(str(save / "scoped.ckpt-1"), scope_index=21)
+    assert torch.equal(q.Wc, p.Wc)
+
+
+def test_save_cadence_matches_reference():
+    """train.py:330: (e * num_batches + b) % save_every == 0."""
+    due = [(e, b) for e in range(3) for b in range(7) if ck.save_due(e, b, 7, 5)]
+    assert due == [(0, 0), (0, 5), (1, 3), (2, 1), (2, 6)]
+
+
+def test_load_reference_checkpoint_copy():
+    """load_params on the reference's own variables (model copy 289 of
+    save/g2k_mcrAttn_model_kfold_train_4_0.ckpt-79): D = 10 shapes, values
+    as stored (float64 -> float32), pedestrian axis padded with zeros."""
+    raw = ck.read_bundle(MCRATTN)
+    q = ck.load_params(MCRATTN, nmax=5)
+    assert tuple(q.Wv.shape) == (8, 12) and tuple(q.bv.shape) == (10,)
+    assert tuple(q.Wii.shape) == (10, 8) and tuple(q.Wr.shape) == (8, 2) and tuple(q.Wc.shape) == (24, 8)
+    assert tuple(q.Wi.shape) == (5, 10) and tuple(q.Wo.shape) == (8, 5)   # stored [0, 10] / [8, 0]
+    assert not q.Wi.any() and not q.Wo.any()
+    assert np.array_equal(q.Wv.numpy(), raw["krnl_weights_289/weight_v"].astype(np.float32))
+    assert np.array_equal(q.Wc.numpy(), raw["krnl_weights_289/weight_c"].astype(np.float32))
+    assert np.array_equal(q.Wr.numpy(), raw["krnl_embed_289/weight_r"].astype(np.float32))
+    with pytest.raises(KeyError):
+        ck.load_params(MCRATTN, scope_index=3)
+    with pytest.raises(KeyError):
+        ck.load_params(GOLD)                                  # no krnl_weights scope

@@ -45,9 +45,23 @@ STAMPS = [
     ("  poll_word(c.sTicket, NP);", "  poll_word(c.sTicket, NP);\n  G2K_ST(15, " + P0 + ");"),
     ("  // the small blocks and dWo, entry by entry", "  G2K_ST(16, " + P0 + ");\n  // the small blocks and dWo, entry by entry"),
     ("  rc.store(a.h_out", "  G2K_ST(20, c.wv == 0);\n  rc.store(a.h_out"),
+    ("    scene_producer<NP, GRAD>(a, lay, c);", "  { G2K_ST(17, " + P0 + "); scene_producer<NP, GRAD>(a, lay, c); }"),
+    ("  __syncthreads();                                              // B1: window + weights landed",
+     "  G2K_ST(18, " + P0 + " && fb == 0);\n  __syncthreads();\n  G2K_ST(19, " + P0 + " && fb == 0);"),
     ("      const FrameHeadOut hd =", "      G2K_ST(30 + 3 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n      const FrameHeadOut hd ="),
     ("      if (L < kL && q < 2) {\n        float* m = c.sMring", "      G2K_ST(31 + 3 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n      if (L < kL && q < 2) {\n        float* m = c.sMring"),
     ("        lds_store_flag(c.sFlag + fl, f + 1);\n      }\n", "        lds_store_flag(c.sFlag + fl, f + 1);\n      }\n      G2K_ST(32 + 3 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n"),
+]
+TILE = [
+    ("f32x4 (&dm)[2], f32x4& dWoT) {", "f32x4 (&dm)[2], f32x4& dWoT, const StepArgs& a, const SceneCtx& c) {\n  G2K_ST(40, " + P0 + " && t == 0);"),
+    ("c.nact, t, L, q, acc, lsum, dm, dWoT);", "c.nact, t, L, q, acc, lsum, dm, dWoT, a, c);"),
+    ("  if (pr && n < nact) {", "  G2K_ST(41, " + P0 + " && t == 0);\n  if (pr && n < nact) {"),
+    ("  // errors: d = Y - target", "  G2K_ST(42, " + P0 + " && t == 0);\n  // errors: d = Y - target"),
+    ("    // dY into the scratch [r][n]", "    G2K_ST(43, " + P0 + " && t == 0);\n    // dY into the scratch [r][n]"),
+    ("    wave_lds_sync();\n    // dm += dY", "    G2K_ST(44, " + P0 + " && t == 0);\n    wave_lds_sync();\n    // dm += dY"),
+    ("    wave_lds_sync();                       // scratch reads done", "    G2K_ST(45, " + P0 + " && t == 0);\n    wave_lds_sync();                       // scratch reads done"),
+    ("      poll_flag(c.sMflag + fl, f + 1);         // M of this frame", "      G2K_ST(46, " + P0 + " && t == 0);\n      poll_flag(c.sMflag + fl, f + 1);         // M of this frame"),
+    ("        if (lay.dwo_seq) {\n          asm volatile", "        G2K_ST(47, " + P0 + " && t == 0);\n        if (lay.dwo_seq) {\n          asm volatile"),
 ]
 NO_RECUR = [("  const bool live = a.h_in != nullptr;", "  const bool live = false;")]
 VARIANTS = {
@@ -59,6 +73,9 @@ VARIANTS = {
                               "  if (false) {\n    // the dY entries of other lanes")]},
     "stamps": {SCENE: STAMPS},
     "stamps_norecur": {SCENE: STAMPS + NO_RECUR},
+    "nolsr": {"__flags__": ["-mllvm", "-disable-lsr"]},
+    "stamps_nolsr": {SCENE: STAMPS, "__flags__": ["-mllvm", "-disable-lsr"]},
+    "stamps_tile": {SCENE: STAMPS + TILE},
 }
 
 
@@ -68,6 +85,8 @@ def build_variant(name):
     for f in os.listdir(src):
         shutil.copy(os.path.join(src, f), tmp)
     for fname, reps in VARIANTS[name].items():
+        if fname == "__flags__":
+            continue
         p = os.path.join(tmp, fname)
         s = open(p).read()
         for a, b in reps:
@@ -79,8 +98,8 @@ def build_variant(name):
     for f in sorted(os.listdir(tmp)):
         if f.endswith(".hip"):
             o = os.path.join(tmp, f[:-4] + ".o")
-            subprocess.run([build.HIPCC, *build.FLAGS, "-c", "-o", o, os.path.join(tmp, f)],
-                           check=True)
+            subprocess.run([build.HIPCC, *build.flags_for(f), *VARIANTS[name].get("__flags__", []), "-c", "-o", o,
+                            os.path.join(tmp, f)], check=True)
             objs.append(o)
     subprocess.run([build.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs],
                    check=True)
@@ -120,10 +139,12 @@ def stamps(lib, c, t, dev):
         rel = (r - r[0]) % (1 << 32)
         names = {1: "B2", 2: "heads", 3: "tiles f0", 4: "tiles f1", 5: "tiles f2", 8: "fgrad f0",
                  9: "fgrad f1", 10: "fgrad f2", 12: "chunk sync", 13: "chunk sum", 14: "ticket",
-                 15: "ticket=NP", 16: "dWi done", 20: "recur end"}
+                 15: "ticket=NP", 16: "dWi done", 17: "prod start", 18: "dma waited",
+                 19: "B1", 20: "recur end"}
         print(f"scene {sc} n_active {int(t['n_active'][sc])}: " +
               "  ".join(f"{v}:{rel[k]}" for k, v in names.items() if r[k] != 0))
         print("   producers' tiles done:", " ".join(str(rel[24 + p]) for p in range(8)))
+        print("   last tile 0 (poll, entry, Y, stores, err, dWoT, dM, dWo):", " ".join(str(rel[k]) for k in (46, 40, 41, 42, 43, 44, 45, 47)))
         print("   heads (start, head done, flags):", " ".join(f"({rel[30 + 3 * i]},{rel[31 + 3 * i]},{rel[32 + 3 * i]})" for i in range(3)))
 
 
