@@ -153,10 +153,15 @@ class GridLSTMCell:
         self.W, self.b = other.W, other.b
 
     def __call__(self, inputs, state, stream=None):
+        # tf.contrib GridLSTMCell slices block f from columns [f * skip, f * skip +
+        # feature_size) and requires int((ncol - feature_size) / skip) + 1 blocks:
+        # a 10-column input (sample.py's num_freq_blocks = 10) feeds 2 blocks of
+        # 4 and its last 2 columns are never read
         K = sum(self.num_frequency_blocks)
-        if int(inputs.shape[1]) != K * self.feature_size:
-            raise ValueError(f"inputs must have {K * self.feature_size} columns "
-                             f"({K} blocks of {self.feature_size})")
+        ncol = int(inputs.shape[1])
+        if ncol < self.feature_size or (ncol - self.feature_size) // self.feature_size + 1 != K:
+            raise ValueError(f"inputs with {ncol} columns do not make {K} blocks of {self.feature_size}")
+        inputs = inputs[:, :K * self.feature_size]
         return gridlstm(inputs, state, self.W, self.b, self.peep,
                         feature_size=self.feature_size, num_units=self.num_units, stream=stream)
 

@@ -1,22 +1,142 @@
-"""sample.py entry point (sample.py:85-355): one forward per batch through the
-HIP step (a fresh online graph per batch, framenum 0, time slice of the
-node positions, sample.py:150-164) and get_mean_error (sample.py:21-82) on the
-GPU (g2k_ade_fde_f32 variant 1).
+"""sample.py entry point (sample.py:85-355) at the reference's geometry:
+D = num_freq_blocks (10), one g2k_lstm_mcr forward per batch on the GPU
+(g2k_mcr_forward_f32 at D = 10, the GridLSTM encoder through g2k_gridlstm_f32)
+and get_mean_error (sample.py:21-82) through g2k_ade_fde_f32 variant 1.
 
-  python -m multimodaltraj_2_amd.sample --data_root /path/to/data --test_dataset 2
+  python -m multimodaltraj_2_amd.sample --data_root /path/to/data --test_dataset 2 \\
+      [--save_dir save]          # restore krnl_weights from the latest checkpoint
+
+Per batch (sample.py:137-330):
+  * a fresh online graph at framenum 0, the time slice of the node positions
+    (sample.py:150-164) -> batch_v = ||pos|| [obs_len, n];
+  * weight_i [n, D], weight_ii [D, obs_len] ~ N(0, 1) (:186-195), inputs =
+    weight_ii @ (batch_v @ weight_i) [D, D], vislet_emb = vislet @ weight_i
+    [2, D], vislet_rel = vislet_past * vislet_emb (:141-144, :197-201);
+  * the GridLSTM encoder over inputs with a zero state (:262-269, helper.py:
+    10-75; 2 blocks of 4 of the 10 columns, tf.contrib's slicing) -> ng_output
+    [D, 8];
+  * g2k_lstm_mcr.forward with outputs = [inputs; vislet_emb], ngh = lambda *
+    ng_output (scaled by lambda again inside the model, :102, as the reference
+    feeds it), rel_features = vislet_rel (:297-312);
+  * get_mean_error(complete_traj, targets) (:327-332).
+Weights: krnl_weights / krnl_embed restored from the checkpoint the
+``checkpoint`` state file in --save_dir names (sample.py:213-225;
+checkpoint.load_params), pedestrian columns the checkpoint lacks (its weight_o
+is sized by the saving batch) drawn N(0, 1); without --save_dir all are drawn
+N(0, 1).  Build decision: the reference re-initialises the restored variables
+right after restoring them (:294-296, quirk) — the restore is kept effective
+here.  The static-context branch (:271-290) feeds nothing the prediction reads
+and is not run.  Small glue products (weight_ii @ batch_v @ weight_i, the
+vislet embedding) are torch matmuls on the GPU.
 """
 from __future__ import annotations
 
 import argparse
+import os
 
 import numpy as np
 import torch
 
+from . import checkpoint
 from . import frame_step as fs
+from . import helper
 from . import networkx_graph as nxg
 from .argParser import ArgsParser
 from .load_traj import DataLoader
-from .scenes import build_scene, pack
+from .models.g2k_lstm_mcr import g2k_lstm_mcr
+from .scenes import build_scene
+
+
+def restore_weights(save_dir, device):
+    """The krnl_* variables of the latest checkpoint in save_dir (G2KParams,
+    float32 on device) or None (no state file)."""
+    prefix = checkpoint.read_state(save_dir) if save_dir else None
+    if prefix is None:
+        return None
+    return checkpoint.load_params(prefix, device=device)
+
+
+def model_weights(restored, n, D, T, seed, device):
+    """g2k_lstm_mcr weights for a batch of n pedestrians: the restored ones,
+    weight_o's missing columns (and everything without a checkpoint) N(0, 1)."""
+    rng = np.random.default_rng(seed)
+    draw = lambda shape: torch.from_numpy(rng.standard_normal(shape).astype(np.float32)).to(device)
+    w = dict(weight_v=draw((T, D + 2)), bias_v=draw((D,)), weight_o=draw((T, n)),
+             weight_c=draw((2 * fs.PRED_LEN, T)), weight_r=draw((T, 2)))
+    if restored is not None:
+        if tuple(restored.Wv.shape) != (T, D + 2):
+            raise ValueError(f"checkpoint weight_v {tuple(restored.Wv.shape)} does not match D = {D}")
+        k = min(n, int(restored.Wo.shape[1]))
+        wo = w["weight_o"].clone()
+        wo[:, :k] = restored.Wo[:, :k]
+        w = dict(weight_v=restored.Wv, bias_v=restored.bv, weight_o=wo, weight_c=restored.Wc,
+                 weight_r=restored.Wr)
+    return w
+
+
+def sample_batch(args, sc, vislet_past, restored, device, seed):
+    """One batch of sample.py (see the module docstring).  Returns
+    (ade, fde, vislet_emb, pred [2, 12, n]) — errors from g2k_ade_fde_f32."""
+    D, T = args.num_freq_blocks, args.obs_len
+    n = sc.window.shape[1]
+    rng = np.random.default_rng(seed)
+    tt = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=device)
+    batch_v = np.linalg.norm(sc.window, axis=2)                     # [obs_len, n]
+    weight_i = tt(rng.standard_normal((n, D)))
+    weight_ii = tt(rng.standard_normal((D, batch_v.shape[0])))
+    inputs = weight_ii @ (tt(batch_v) @ weight_i)                   # [D, D]
+    vislet_emb = tt(sc.vislet[:, :n]) @ weight_i                    # [2, D]
+    vislet_rel = vislet_past * vislet_emb
+    enc = helper.neighborhood_vis_loc_encoder(hidden_size=args.rnn_size, hidden_len=D,
+                                              num_layers=args.num_layers, grid_size=args.grid_size,
+                                              embedding_size=args.embedding_size, device=device,
+                                              seed=seed)
+    ng_output, _ = enc.forward(inputs.contiguous(), torch.zeros((D, args.rnn_size), device=device))
+    model = g2k_lstm_mcr(in_features=(D, D), hidden_size=args.rnn_size, obs_len=T, num_nodes=n,
+                         lambda_reg=args.lambda_param, device=device,
+                         weights=model_weights(restored, n, D, T, seed + 1, device))
+    pred = model.forward(dict(outputs=torch.cat([inputs, vislet_emb], 0), ngh=args.lambda_param * ng_output,
+                              rel_features=vislet_rel, out_size=n))
+    nmax = max(n, 1)
+    pr = torch.zeros((1, 2 * fs.PRED_LEN, nmax), device=device)
+    pr[0, :, :n] = model.temp_path
+    tg = torch.zeros((1, nmax, fs.PRED_LEN, 2), device=device)
+    tg[0, :n] = tt(sc.targets)
+    err = fs.ade_fde(pr, tg, torch.tensor([n], dtype=torch.int32, device=device), variant=1,
+                     obs_length=args.obs_length)
+    e = err[0].cpu().numpy()
+    return float(e[0]), float(e[1]), vislet_emb, pred
+
+
+def batches(args, loader):
+    """sample.py:137-164 / 318-320: (scene, targets present) per batch."""
+    for b in range(loader.num_batches):
+        batch, tgt, _ = loader.next_step()
+        if len(batch) == 0:
+            break
+        g = nxg.online_graph(args).ConstructGraph(current_batch=batch, framenum=0, future_traj=tgt)
+        sc = build_scene(batch, tgt, g, loader, 0, mode="sample")
+        node_t = g.get_node_attr("targets")
+        try:
+            y = np.stack([np.asarray(v[0], np.float64) for v in node_t.values()])
+        except ValueError:
+            continue                                       # ragged targets: np.stack fails too
+        if y.ndim != 3 or y.shape[1] < fs.PRED_LEN or sc.window.shape[1] < 1:
+            continue
+        sc.targets = y[:sc.window.shape[1], :fs.PRED_LEN]
+        yield b, sc
+
+
+def run(args, loader, device, log=print):
+    restored = restore_weights(args.save_dir, device)
+    vislet_past = 1.0
+    total, final = [], []
+    for b, sc in batches(args, loader):
+        ade, fde, vislet_past, _ = sample_batch(args, sc, vislet_past, restored, device, args.seed)
+        total.append(ade)
+        final.append(fde)
+        log(f"batch {b}: ADE {ade:.4f} FDE {fde:.4f} peds {sc.window.shape[1]}")
+    return total, final
 
 
 def main(argv=None):
@@ -31,38 +151,9 @@ def main(argv=None):
     loader = DataLoader(args, datasets=[0, 1, 2, 3, 4, 5], start=args.test_dataset, sel=0,
                         data_root=args.data_root)
     loader.reset_data_pointer()
-    H = args.rnn_size
-    total, final = [], []
-    for b in range(loader.num_batches):
-        batch, tgt, _ = loader.next_step()
-        if len(batch) == 0:
-            break
-        g = nxg.online_graph(args).ConstructGraph(current_batch=batch, framenum=0, future_traj=tgt)
-        sc = build_scene(batch, tgt, g, loader, 0, mode="sample")
-        node_t = g.get_node_attr("targets")
-        try:
-            y = np.stack([np.asarray(v[0], np.float64) for v in node_t.values()])
-        except ValueError:
-            continue                                       # ragged targets: np.stack fails too
-        if y.ndim != 3 or y.shape[1] < 12:
-            continue
-        sc.targets = y[:, :12]
-        sc.mask[:] = True
-        sc.n_frames = 1
-        pk = pack([sc], H)
-        params = fs.init_params(pk["Nmax"], seed=args.seed, device=device)
-        t = {k: torch.from_numpy(v).to(device) for k, v in pk.items() if isinstance(v, np.ndarray)}
-        G = torch.from_numpy(np.random.default_rng(args.seed + 1).standard_normal(
-            (1, 16, 8)).astype(np.float32)).to(device)
-        h = torch.zeros((1, 16, H), device=device)
-        out = fs.step_fused(params, t["pos"], t["vislet"], G, t["targets"], t["n_active"], h,
-                            n_frames=t["n_frames"], stride=0, lam=args.lambda_param)
-        err = fs.ade_fde(out.pred[:, 0].contiguous(), t["targets"][:, 0].contiguous(),
-                         t["n_active"], variant=1, obs_length=args.obs_length)
-        e = err[0].cpu().numpy()
-        total.append(float(e[0]))
-        final.append(float(e[1]))
-        print(f"batch {b}: ADE {e[0]:.4f} FDE {e[1]:.4f} peds {sc.window.shape[1]}")
+    if args.save_dir and not os.path.exists(os.path.join(args.save_dir, "checkpoint")):
+        print(f"no checkpoint state file in {args.save_dir}: weights drawn N(0, 1)")
+    total, final = run(args, loader, device)
     if total:
         print("Total mean error of the model is ", np.mean(total))
         print("Total final error of the model is ", np.mean(final))

@@ -100,3 +100,13 @@ def test_encoders_on_checkpoint_weights(gpu):
     r2, q2 = ref.gridlstm_cell(xs, h, z["W"], z["b"], None)
     assert o2.shape == (16, 8)
     assert close(o2.cpu().numpy(), r2) <= TOL and close(s2.cpu().numpy(), q2) <= TOL
+
+
+def test_tf_block_slicing_rule():
+    """tf.contrib GridLSTMCell: int((ncol - feature_size) / skip) + 1 blocks;
+    sample.py's 10-column input makes 2 blocks of 4 (columns 8, 9 unread)."""
+    cell = helper.GridLSTMCell(2, 4, 4, True, [2], device="cpu")
+    with pytest.raises(ValueError):
+        cell(torch.zeros(10, 7), torch.zeros(10, 8))
+    with pytest.raises(ValueError):
+        cell(torch.zeros(10, 12), torch.zeros(10, 8))

@@ -98,3 +98,62 @@ def test_real_data_plumbing(gpu, name, mode):
         assert close(out.pred[s, :nf, :, :n].cpu().numpy().reshape(nf, 2, 12, n), pr) <= TOL
         assert close(out.h[s].cpu().numpy(), h) <= TOL
         assert close(out.metrics[s, :6].cpu().numpy(), m[:6]) <= TOL
+
+
+MCRATTN = os.path.join(GOLDEN, "ckpt_mcrattn_289")
+
+
+def test_g2k_lstm_mcr_d10_on_reference_checkpoint(gpu):
+    """sample.py's geometry (D = num_freq_blocks = 10) on the reference's own
+    weights (model copy 289 of save/g2k_mcrAttn_model_kfold_train_4_0.ckpt-79:
+    weight_v [8, 12], bias_v [10], weight_c [24, 8], weight_r [8, 2]) through
+    g2k_mcr_forward_f32; the checkpoint's weight_o is [8, 0] (its last batch
+    had no pedestrians), so 7 seeded columns stand in."""
+    from multimodaltraj_2_amd.models.g2k_lstm_mcr import checkpoint_weights
+    w = checkpoint_weights(MCRATTN, num_nodes=7, device=gpu)
+    w["weight_o"] = torch.from_numpy(np.random.default_rng(3).standard_normal((8, 7)).astype(np.float32)).to(gpu)
+    m = g2k_lstm_mcr(in_features=torch.zeros(10, 10), hidden_size=128, obs_len=8, num_nodes=7,
+                     lambda_reg=5e-4, sess_g=None, device=gpu, weights=w)
+    rng = np.random.default_rng(11)
+    feed = dict(outputs=rng.standard_normal((12, 10)), ngh=rng.standard_normal((10, 8)),
+                rel_features=rng.standard_normal((2, 10)) ** 2, out_size=7)
+    pred = m.forward(feed).cpu().numpy()
+    cpu = {k: v.cpu().numpy().astype(np.float64) for k, v in w.items()}
+    o = ref.mcr_forward(feed["outputs"].astype(np.float32), feed["rel_features"].astype(np.float32),
+                        feed["ngh"].astype(np.float32), cpu["weight_v"], cpu["bias_v"], cpu["weight_r"],
+                        cpu["weight_c"], cpu["weight_o"], 5e-4)
+    assert pred.shape == (2, 12, 7) and tuple(m.attn.shape) == (10, 10)
+    assert close(pred, o["pred_path_band"]) <= TOL
+    assert close(m.cost.cpu().numpy(), o["cost"]) <= TOL
+    assert close(m.attn.cpu().numpy(), o["attn"]) <= TOL
+
+
+def test_wc_cost_known_answer_through_hip(gpu):
+    """The reference's stored forward product Variable [24, 8] == weight_c @
+    cost (models/g2k_lstm_mcr.py:122; bit-exact in its checkpoint for this
+    copy) reproduced by g2k_mcr_forward_f32 at D = 10: outputs chosen so that
+    E = weight_v @ outputs + bias_v = [I_8 | 0], ngh = [cost; 0] and
+    weight_o = I_8, so the kernel's pred_path_band is weight_c @ cost."""
+    t = ck_read(MCRATTN)
+    Wv, bv = t["krnl_weights_289/weight_v"], t["krnl_weights_289/bias_v"]
+    Wc, cost, known = t["krnl_weights_289/weight_c"], t["Variable_1737"], t["Variable_1738"]
+    assert np.abs(Wc @ cost - known).max() < 1e-12          # the stored known answer itself
+    E = np.zeros((8, 10))
+    E[:, :8] = np.eye(8)
+    X = np.linalg.pinv(Wv) @ (E - bv[None, :])              # weight_v [8, 12] has full row rank
+    G = np.zeros((10, 8))
+    G[:8] = cost
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(gpu)   # noqa: E731
+    params = fs.G2KParams(Wi=torch.zeros((8, 10), device=gpu), Wii=torch.zeros((10, 8), device=gpu),
+                          Wv=dev(Wv), bv=dev(bv), Wr=dev(t["krnl_embed_289/weight_r"]), Wc=dev(Wc),
+                          Wo=dev(np.eye(8)))
+    attn, c, pred = fs.mcr_forward(params, dev(X)[None], dev(np.ones((2, 10)))[None], dev(G)[None],
+                                   torch.tensor([8], dtype=torch.int32, device=gpu), lam=1.0)
+    torch.cuda.synchronize()
+    assert close(c[0].cpu().numpy(), cost) <= 1e-5
+    assert close(pred[0].cpu().numpy(), known) <= 1e-5
+
+
+def ck_read(prefix):
+    from multimodaltraj_2_amd.checkpoint import read_bundle
+    return read_bundle(prefix)
