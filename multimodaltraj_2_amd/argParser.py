@@ -35,6 +35,9 @@ class ArgsParser:
                         help="batch_v slice: train.py node slice (Q10) or sample.py time slice")
     parser.add_argument('--chain_hidden', type=int, default=1,
                         help='carry hidden_state from batch to batch like train.py')
+    parser.add_argument('--valid_from_seed', type=int, default=0,
+                        help="validation leg from the file's first frame (the reference starts "
+                             "at frame 0, which the ETH/UCY frame keys never hit)")
     parser.add_argument('--log_dir', type=str, default='log')
     parser.add_argument('--seed', type=int, default=0)
     parser.add_argument('--save_dir', type=str, default='',
