@@ -45,6 +45,7 @@ from multimodaltraj_2_amd.synthetic import CONFIGS, FRAMES_PER_SCENE, make_batch
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MALL_BYTES = 256 * 2 ** 20     # Infinity Cache: rotate past this many bytes
 METRIC = "frames/sec (obs=8,pred=12) g2k_lstm_mcr train step; ADE/FDE vs reference"
+REAL = "eth_ucy_real"          # config 3's workload on real data (multimodaltraj_2_amd/realdata.py)
 
 
 # ---------------------------------------------------------------------------
@@ -56,10 +57,12 @@ def algorithmic_bytes(b, H, params_bytes):
     the weights; writes pred for the active columns (padded columns are not
     written), h_out and the metrics row."""
     S, W, Nmax, _ = b.pos.shape
-    F, L2, D, T = b.F, 24, 16, 8
+    L2, D, T = 24, 16, 8
+    F = b.n_frames.astype(np.int64) if b.n_frames is not None else b.F
     nact = b.n_active.astype(np.int64)
+    extra = S * 4 + S * Nmax if b.n_frames is not None else 0      # n_frames, ped_mask
     rd = (W * nact * 8).sum() + (2 * nact * 4).sum() + S * D * T * 4 \
-        + (F * nact * L2 * 4).sum() + S * D * H * 4 + S * 4 + params_bytes
+        + (F * nact * L2 * 4).sum() + S * D * H * 4 + S * 4 + params_bytes + extra
     wr = (F * L2 * nact * 4).sum() + S * D * H * 4 + S * 8 * 4
     return int(rd + wr)
 
@@ -97,9 +100,11 @@ def _oracle_scenes(b, params_np, lo, hi, budget_s, threads):
         t0 = time.perf_counter()
         s = lo
         while True:
+            nf = int(b.n_frames[s]) if b.n_frames is not None else b.F
+            pm = b.ped_mask[s].astype(bool) if b.ped_mask is not None else None
             ref.scene_step(b.pos[s], b.vislet[s], b.G[s], params_np, b.targets[s],
-                           b.n_active[s], b.h0[s], n_frames=b.F, stride=b.stride)
-            frames += b.F
+                           b.n_active[s], b.h0[s], n_frames=nf, stride=b.stride, ped_mask=pm)
+            frames += nf
             s = s + 1 if s + 1 < hi else lo
             if time.perf_counter() - t0 > budget_s:
                 break
@@ -107,10 +112,7 @@ def _oracle_scenes(b, params_np, lo, hi, budget_s, threads):
 
 
 def _pool_worker(a):
-    cfg, seed, lo, hi, budget = a
-    c = CONFIGS[cfg]
-    b = make_batch(hi, c["Nmax"], c["H"], F=FRAMES_PER_SCENE, seed=seed)
-    p = fs.init_params(c["Nmax"], seed=0).numpy()
+    b, p, lo, hi, budget = a
     return _oracle_scenes(b, p, lo, hi, budget, 1)
 
 
@@ -124,7 +126,7 @@ def cpu_baseline(cfg, b, params_np, budget_s, procs):
     f1, t1 = _oracle_scenes(b, params_np, 0, S, budget_s, 1)
     fa, ta = _oracle_scenes(b, params_np, 0, S, budget_s / 2, None)
     per = max(1, S // procs)
-    jobs = [(cfg, 1, (i * per) % S, min(S, (i * per) % S + per), budget_s / 2)
+    jobs = [(b, params_np, (i * per) % S, min(S, (i * per) % S + per), budget_s / 2)
             for i in range(procs)]
     ctx = mp.get_context("spawn")
     with ctx.Pool(procs) as pool:
@@ -132,7 +134,7 @@ def cpu_baseline(cfg, b, params_np, budget_s, procs):
     agg = sum(f for f, _ in res) / max(t for _, t in res)
     return {"value": f1 / t1, "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": f"the float64 NumPy oracle (oracle/g2k_ref.py) in train.py's per-scene loop, "
-                      f"{f1 // b.F} scenes x {b.F} frames of the same workload in {t1:.1f} s, "
+                      f"{f1} frames of the same workload's scenes in {t1:.1f} s, "
                       f"1 thread (the reference's TF path cannot run here: no TF 1.x)",
             "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
             "blas_all_threads": {"value": fa / ta, "unit": "frames/s", "seconds": round(ta, 2)},
@@ -238,7 +240,7 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="eth_hotel_synth", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="eth_hotel_synth", choices=sorted(CONFIGS) + [REAL])
     ap.add_argument("--scenes", type=int, default=0, help="override scenes per rank")
     ap.add_argument("--rotate", type=int, default=0,
                     help="input batches to rotate over (0: enough to exceed the 256 MiB MALL)")
@@ -260,12 +262,18 @@ def main(argv=None):
     if args.selftest_launcher:
         return selftest_worker(args, world, rank)
 
-    cfg = dict(CONFIGS[args.config])
-    if args.config in ("eth_ucy_loo_kfold4", "dense_crowd"):
-        cfg["S"] = cfg["S"] // 8          # 128 scenes per GPU
-    S = args.scenes or cfg["S"]
-    Nmax, H, F = cfg["Nmax"], cfg["H"], FRAMES_PER_SCENE
-    b = make_batch(S, Nmax, H, F=F, seed=1 + rank)
+    if args.config == REAL:
+        from multimodaltraj_2_amd.realdata import real_batch
+        S, H = args.scenes or 128, 128
+        b = real_batch(S, H, seed=1 + rank)
+        Nmax, F = b.pos.shape[2], b.F
+    else:
+        cfg = dict(CONFIGS[args.config])
+        if args.config in ("eth_ucy_loo_kfold4", "dense_crowd"):
+            cfg["S"] = cfg["S"] // 8          # 128 scenes per GPU
+        S = args.scenes or cfg["S"]
+        Nmax, H, F = cfg["Nmax"], cfg["H"], FRAMES_PER_SCENE
+        b = make_batch(S, Nmax, H, F=F, seed=1 + rank)
     params_host = fs.init_params(Nmax, seed=0)
 
     # CPU baseline first: its worker processes are spawned before this
@@ -304,7 +312,8 @@ def main(argv=None):
                              metrics=torch.empty((S, 8), device=dev))
         batches.append(t)
         plans.append(fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"],
-                                 t["n_active"], t["h0"], out=out))
+                                 t["n_active"], t["h0"], n_frames=t["n_frames"],
+                                 ped_mask=t["ped_mask"], stride=b.stride, out=out))
 
     def step(i):
         plans[i % K].run()
@@ -327,7 +336,7 @@ def main(argv=None):
         m = tot.cpu().numpy()
         line = {
             "metric": METRIC,
-            "value": S * F * world * args.steps / elapsed,
+            "value": b.frames * world * args.steps / elapsed,
             "unit": "frames/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -337,11 +346,14 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded random-walk ETH-shaped scenes; N(0,1) weights)",
+            "data": ("real (ETH/UCY batches of the reference's data files, train.py batch walk, "
+                     "stride 0, n_frames = len(batch); N(0,1) weights)" if args.config == REAL else
+                     "synthetic (seeded random-walk ETH-shaped scenes; N(0,1) weights)"),
             "mode": "reference (train.py:197-276: forward, recurrence, ADE/FDE; the reference "
                     "has no backward)",
             "config": {"workload": args.config, "scenes_per_gpu": S, "global_scenes": S * world,
-                       "frames_per_scene": F, "obs_len": 8, "pred_len": 12, "Nmax": Nmax,
+                       "frames_per_scene": F if b.n_frames is None else float(b.n_frames.mean()),
+                       "frames_per_step": b.frames, "obs_len": 8, "pred_len": 12, "Nmax": Nmax,
                        "hidden": H, "D": 16, "parallelism": f"dp{world}",
                        "input_batches_rotated": K},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -373,9 +385,10 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K):
     from multimodaltraj_2_amd.train_step import TrainStep
     t0 = batches[0]
     ts = TrainStep(params, t0["pos"], t0["vislet"], t0["G"], t0["targets"], t0["n_active"],
-                   t0["h0"])
+                   t0["h0"], n_frames=t0["n_frames"], ped_mask=t0["ped_mask"], stride=b.stride)
     for t in batches[1:]:
-        ts.bind(t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+        ts.bind(t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
+                n_frames=t["n_frames"], ped_mask=t["ped_mask"])
     last = {}
 
     def step(i):
@@ -388,7 +401,7 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K):
     achieved = abytes / kern_s / 1e9
     return {"metric": "frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + L2 loss gradient + "
                       "gradient all-reduce + RMSProp update",
-            "value": S * F * world * args.steps / el, "unit": "frames/s",
+            "value": b.frames * world * args.steps / el, "unit": "frames/s",
             "ms_per_step": el / args.steps * 1e3, "allreduce_bytes": int((ts.P + 2) * 4),
             "loss_per_prediction_last_step": float(gl[-2] / max(gl[-1], 1.0)),
             "optimizer": "RMSProp lr 0.005 decay 0.95, global-norm clip 10 (argParser.py:38-47)",

@@ -79,11 +79,15 @@ class DataLoader:
         """load_traj.py:234-256: {frame: [{ped: [x, y]}, ...]}; every frame of
         frameList is a key (empty dict), frames seed + k*diff get their peds."""
         frame_data = {i: {} for i in self.frameList}
-        ppfl = np.transpose(self.pedsPerFrameList)
+        # the rows of each frame index in file order, grouped in one pass (the
+        # reference rescans every row per frame: same lists, O(rows) here)
+        rows = {}
+        for (ind, ped, px, py) in np.transpose(self.pedsPerFrameList):
+            rows.setdefault(ind, []).append({ped: [px, py]})
         fp = self.frame_pointer
-        fmax = max(self.frameList)
+        fmax = self._fmax = max(self.frameList)
         while fp <= fmax:
-            frame_data[fp] = [{ped: [px, py]} for (ind, ped, px, py) in ppfl if ind == fp]
+            frame_data[fp] = rows.get(fp, [])
             fp += self.diff
         return frame_data
 
@@ -102,7 +106,7 @@ class DataLoader:
         tgt = {} if targets is None else targets
         batch, window = {}, {}
         visits = 1                                   # `pc`, kept across passes
-        fmax = max(self.frameList)
+        fmax = self._fmax
         last = self.frame_pointer
         span = self.batch_size * self.obs_len
         for _ in range(self.batch_size + 1):

@@ -38,6 +38,13 @@ class SceneBatch:
     n_active: np.ndarray   # [S] int32
     h0: np.ndarray         # [S, D, H]
     stride: int = 1
+    n_frames: np.ndarray | None = None   # [S] int32 (real data: len(batch)); None: all F
+    ped_mask: np.ndarray | None = None   # [S, Nmax] uint8 (real data); None: all active
+
+    @property
+    def frames(self) -> int:
+        """Frames one step processes (the metric's unit)."""
+        return int(self.n_frames.sum()) if self.n_frames is not None else self.S * self.F
 
     @property
     def S(self):

@@ -33,3 +33,20 @@ def test_context_conv_matches_oracle(gpu, h, w, c, dim):
     rG = ref.context_input(rc, ref.static_mask(dim, 8))
     assert np.abs(conv.cpu().numpy() - rc).max() <= 1e-4 * np.abs(rc).max()
     assert np.abs(G.cpu().numpy() - rG).max() <= 1e-4 * np.abs(rG).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim", [16, 10])
+def test_context_conv_full_frame(gpu, dim):
+    """The reference's frame size (576 x 720 x 3, padded to 578 x 721,
+    train.py:95-110): a 563 x 706 x 3 filter at D = 16 (569 x 712 at D = 10)."""
+    rng = np.random.default_rng(dim)
+    img = rng.uniform(0, 255, size=(576, 720, 3)).astype(np.float32)
+    filt = rng.standard_normal(context.context_filter_shape(576, 720, 3, dim)).astype(np.float32)
+    conv, G = context.static_context(torch.from_numpy(img).to(gpu), torch.from_numpy(filt).to(gpu),
+                                     dim=dim, lam=5e-4)
+    torch.cuda.synchronize()
+    rc = ref.context_conv(img, filt, dim, 5e-4)
+    rG = ref.context_input(rc, ref.static_mask(dim, 8))
+    assert np.abs(conv.cpu().numpy() - rc).max() <= 1e-4 * np.abs(rc).max()
+    assert np.abs(G.cpu().numpy() - rG).max() <= 1e-4 * np.abs(rG).max()
