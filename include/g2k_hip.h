@@ -263,6 +263,30 @@ int g2k_step_grad_update_f32(const g2k_dims* d, const g2k_weights* w, const floa
  *   out  [D, D] or NULL                 G [D, T = 8] or NULL (one must be set)
  *   D in 1..16; workspace >= g2k_context_conv_workspace_bytes(Hh, Ww, D).
  */
+/*
+ * Bivariate-Gaussian NLL head and sampling path (the
+ * reference has no such head: the build's, parity unpinned — oracle/g2k_ref.py
+ * restates it and pins the gradient by central finite differences).
+ * head [3][12] = {log sigma_x[t], log sigma_y[t], atanh rho[t]} around
+ * mu = pred (pred [S, F, 2L, Nmax] as g2k_step_fused_f32 writes it; targets
+ * [S, F, Nmax, L, 2], 8-byte aligned; n_frames / ped_mask may be NULL).
+ * g2k_nll_f32: out [38] = {d nll / d head (36, head order), nll summed over
+ *   frames < n_frames, active masked pedestrians and the 12 steps, count of
+ *   (frame, pedestrian) pairs}, fixed reduction order; dpred (or NULL) =
+ *   d nll / d pred for those pairs, zero for the other active columns of
+ *   frames < n_frames.  workspace >= g2k_nll_workspace_bytes(d).
+ * g2k_gauss_sample_f32: out [S, F, 2L, Nmax] = one draw per (step, pedestrian)
+ *   from the head's Gaussian around pred (Box-Muller over a counter-based
+ *   hash of seed and the element index: reproducible).  Reads d->S, F, Nmax.
+ */
+int64_t g2k_nll_workspace_bytes(const g2k_dims* d);
+int g2k_nll_f32(const g2k_dims* d, const float* pred, const float* targets,
+                const int32_t* n_active, const int32_t* n_frames, const uint8_t* ped_mask,
+                const float* head, float* out, float* dpred, void* workspace,
+                int64_t workspace_bytes, void* stream);
+int g2k_gauss_sample_f32(const g2k_dims* d, const float* pred, const float* head, uint64_t seed,
+                         float* out, void* stream);
+
 int64_t g2k_context_conv_workspace_bytes(int32_t Hh, int32_t Ww, int32_t D);
 int g2k_context_conv_f32(const float* img, int32_t Hh, int32_t Ww, int32_t C, const float* filt,
                          int32_t D, float lambda, float* out, float* G, void* workspace,

@@ -53,6 +53,11 @@ SYMBOLS = {
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp,
                                   c_i64, c_vp]),
     "g2k_update_f32": (c_int, [c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_vp]),
+    "g2k_nll_workspace_bytes": (c_i64, [ctypes.POINTER(G2KDims)]),
+    "g2k_nll_f32": (c_int, [ctypes.POINTER(G2KDims), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                            c_vp, c_i64, c_vp]),
+    "g2k_gauss_sample_f32": (c_int, [ctypes.POINTER(G2KDims), c_vp, c_vp, ctypes.c_uint64, c_vp,
+                                     c_vp]),
     "g2k_step_grad_update_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
                                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp,
                                          c_vp, c_i64, c_vp, c_vp, c_f32, c_f32, c_f32, c_vp]),

@@ -303,6 +303,55 @@ int g2k_step_grad_update_f32(const g2k_dims* d, const g2k_weights* w, const floa
                       (hipStream_t)stream);
 }
 
+static int validate_nll(const g2k_dims* d, const float* pred, const float* head,
+                        const int32_t* n_active) {
+  if (!d) return set_err(G2K_EINVAL, "dims is NULL");
+  if (d->T != kT || d->L != kL) return set_err(G2K_EUNSUPPORTED, "T=%d L=%d (8, 12)", d->T, d->L);
+  if (d->S < 0 || d->F < 0 || d->Nmax < 1 || d->Nmax > kMaxN)
+    return set_err(G2K_EINVAL, "S=%d F=%d Nmax=%d", d->S, d->F, d->Nmax);
+  if (!pred || !head || !n_active) return set_err(G2K_EINVAL, "a required buffer pointer is NULL");
+  return G2K_OK;
+}
+
+int64_t g2k_nll_workspace_bytes(const g2k_dims* d) {
+  if (!d || d->S < 0) return -1;
+  return (int64_t)d->S * (3 * kL + 2) * 4;
+}
+
+int g2k_nll_f32(const g2k_dims* d, const float* pred, const float* targets,
+                const int32_t* n_active, const int32_t* n_frames, const uint8_t* ped_mask,
+                const float* head, float* out, float* dpred, void* workspace,
+                int64_t workspace_bytes, void* stream) {
+  int rc = validate_nll(d, pred, head, n_active);
+  if (rc) return rc;
+  if (!targets || !out) return set_err(G2K_EINVAL, "a required buffer pointer is NULL");
+  if (((uintptr_t)targets) & 7) return set_err(G2K_EINVAL, "targets must be 8-byte aligned");
+  const int64_t need = g2k_nll_workspace_bytes(d);
+  if (!workspace || workspace_bytes < need)
+    return set_err(G2K_EINVAL, "workspace of %lld bytes needed (got %lld)", (long long)need,
+                   (long long)workspace_bytes);
+  hipStream_t st = (hipStream_t)stream;
+  if (d->S == 0) {
+    if (hipMemsetAsync(out, 0, (3 * kL + 2) * 4, st) != hipSuccess)
+      return set_err(G2K_ELAUNCH, "nll: memset failed");
+    return G2K_OK;
+  }
+  float* rows = static_cast<float*>(workspace);
+  if ((rc = nll_launch(d, pred, targets, n_active, n_frames, ped_mask, head, rows, dpred, st)))
+    return rc;
+  return grad_rows_launch(rows, d->S, 3 * kL + 2, out, st);
+}
+
+int g2k_gauss_sample_f32(const g2k_dims* d, const float* pred, const float* head, uint64_t seed,
+                         float* out, void* stream) {
+  int32_t one = 1;
+  int rc = validate_nll(d, pred, head, &one);
+  if (rc) return rc;
+  if (!out) return set_err(G2K_EINVAL, "out is NULL");
+  if ((int64_t)d->S * d->F * kL * d->Nmax == 0) return G2K_OK;
+  return gauss_sample_launch(d, pred, head, seed, out, (hipStream_t)stream);
+}
+
 int g2k_update_f32(float* params, float* ms, const float* grad, int64_t n_params, float lr,
                    float decay, float grad_clip, void* stream) {
   if (!params || !grad || n_params < 0 || n_params > (1 << 30))

@@ -362,6 +362,13 @@ int grad_rows_launch(const float* rows, int S, int width, float* grad, hipStream
 int update_launch(float* params, float* ms, const float* grad, int n, float lr, float decay,
                   float clip, hipStream_t st);
 
+// g2k_nll.hip
+int nll_launch(const g2k_dims* d, const float* pred, const float* targets, const int32_t* n_active,
+               const int32_t* n_frames, const uint8_t* ped_mask, const float* head, float* rows,
+               float* dpred, hipStream_t st);
+int gauss_sample_launch(const g2k_dims* d, const float* pred, const float* head, uint64_t seed,
+                        float* out, hipStream_t st);
+
 // g2k_ops.hip
 int recur_launch(const float* A, float* h, int S, int frames, int D, int H, hipStream_t st);
 int mcr_forward_launch(const g2k_dims* d, const g2k_weights* w, const float* X, const float* Rel,
