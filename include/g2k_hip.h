@@ -237,9 +237,12 @@ int g2k_train_step_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
  *   the same launch (the producers turn each prediction tile's error into the
  *   loss gradient; nothing is recomputed), then the per-scene gradient rows
  *   summed in a fixed order; with params != NULL (one rank) also the update
- *   of g2k_update_f32 (ms NULL: SGD).  Across ranks: call with params NULL,
- *   all-reduce grad, then g2k_update_f32.  workspace >=
- *   g2k_train_workspace_bytes(d) (one gradient row per scene).
+ *   of g2k_update_f32 (ms NULL: SGD), run by the summing launch's last
+ *   workgroup (two launches per step; same results bit for bit as the
+ *   separate update).  Across ranks: call with params NULL, all-reduce grad,
+ *   then g2k_update_f32.  workspace >= g2k_train_workspace_bytes(d) (one
+ *   gradient row per scene and a 64-byte ticket line; no initialisation
+ *   needed).
  * g2k_step_grad_update_f32: one rank's whole train-mode update (nothing to
  *   all-reduce): g2k_step_grad_f32 then g2k_update_f32 on params [P] (the flat
  *   buffer in g2k_weights order, P = g2k_grad_size) with the last reduction

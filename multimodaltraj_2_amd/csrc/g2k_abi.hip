@@ -89,8 +89,9 @@ StepArgs step_args(const g2k_dims* d, const g2k_weights* w, const float* pos, co
   return a;
 }
 
+// [S][P + 2] gradient rows, then one 64-byte line for the update ticket
 int64_t grad_rows_bytes(const g2k_dims* d) {
-  return (int64_t)d->S * (grad_params(d->Nmax) + 2) * 4;
+  return (int64_t)d->S * (grad_params(d->Nmax) + 2) * 4 + 64;
 }
 
 // train mode after the inputs are validated: the fused step with gradient
@@ -109,13 +110,15 @@ int train_launch(StepArgs a, float* grad, void* workspace, int64_t workspace_byt
     if (hipMemsetAsync(grad, 0, (size_t)width * 4, st) != hipSuccess)
       return set_err(G2K_ELAUNCH, "train step: memset failed");
     if (a.d.S > 0 && a.h_in && (rc = scene_step_launch(a, st))) return rc;   // forward outputs
-  } else {
-    a.grad_rows = static_cast<float*>(workspace);
-    if ((rc = scene_step_launch(a, st))) return rc;
-    if ((rc = grad_rows_launch(a.grad_rows, a.d.S, width, grad, st))) return rc;
+    if (params) return update_launch(params, ms, grad, width - 2, lr, decay, grad_clip, st);
+    return G2K_OK;
   }
-  if (params) return update_launch(params, ms, grad, width - 2, lr, decay, grad_clip, st);
-  return G2K_OK;
+  a.grad_rows = static_cast<float*>(workspace);
+  a.grad_ticket = params ? reinterpret_cast<int*>(a.grad_rows + (size_t)a.d.S * width) : nullptr;
+  if ((rc = scene_step_launch(a, st))) return rc;
+  if (!params) return grad_rows_launch(a.grad_rows, a.d.S, width, grad, st);
+  const UpdateArgs up{params, ms, lr, decay, grad_clip, a.grad_ticket};
+  return grad_rows_launch(a.grad_rows, a.d.S, width, grad, st, &up);
 }
 
 }  // namespace

@@ -351,6 +351,8 @@ struct StepArgs {
   float* cost_out;
   float lambda;
   float* grad_rows;   // [S][P + 2] or NULL
+  int* grad_ticket;   // train step with update: zeroed by workgroup 0 for the gradient-row
+                      // sum's last-workgroup count (g2k_train.hip), or NULL
 };
 int scene_step_launch(const StepArgs& a, hipStream_t st);
 int64_t scene_lds_bytes(const g2k_dims* d, bool grad);
@@ -358,7 +360,16 @@ int64_t scene_lds_bytes(const g2k_dims* d, bool grad);
 __host__ __device__ inline int grad_params(int Nmax) { return 24 * Nmax + 496; }
 
 // g2k_train.hip
-int grad_rows_launch(const float* rows, int S, int width, float* grad, hipStream_t st);
+// the optimizer step folded into the gradient-row sum (run by the workgroup
+// that finishes last; `ticket` zeroed by the same step's scene kernel)
+struct UpdateArgs {
+  float* params;
+  float* ms;
+  float lr, decay, clip;
+  int* ticket;
+};
+int grad_rows_launch(const float* rows, int S, int width, float* grad, hipStream_t st,
+                     const UpdateArgs* up = nullptr);
 int update_launch(float* params, float* ms, const float* grad, int n, float lr, float decay,
                   float clip, hipStream_t st);
 

@@ -1161,6 +1161,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket
   if (GRAD) {                                          // accumulators and their sequence words
     for (int i = c.tid; i < lay.o_gseq + rup4(2 + c.ntiles) - lay.o_gacc; i += NT) smem[lay.o_gacc + i] = 0.f;
+    if (a.grad_ticket && c.s == 0 && c.tid == 0) *a.grad_ticket = 0;   // this step's update ticket
   }
   if (F > 0) {
     // issued before n_active / n_frames arrive: the first chunk's window for

@@ -193,7 +193,7 @@ class TrainStep:
     parameters and optimizer state.  The RMSProp mean squares start at one,
     as TF's RMSPropOptimizer initialises its "rms" slot."""
 
-    kernel_names = "g2k_scene_kernel<GRAD> + g2k_grad_rows_kernel + g2k_update_kernel"
+    kernel_names = "g2k_scene_kernel<GRAD> + g2k_grad_rows_kernel<update> (one rank)"
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
                  lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,

@@ -95,8 +95,9 @@ def test_gridlstm_and_train_entry_points_validate():
     d = _dims()
     assert lib.g2k_grad_size(ctypes.byref(d)) == 24 * 32 + 496
     need = lib.g2k_grad_workspace_bytes(ctypes.byref(d))
-    # one gradient row [P + 2] per scene (the fused kernel's output)
-    assert need == 2 * (24 * 32 + 498) * 4
+    # one gradient row [P + 2] per scene (the fused kernel's output), then
+    # the 64-byte line of the folded update's ticket
+    assert need == 2 * (24 * 32 + 498) * 4 + 64
     assert lib.g2k_train_workspace_bytes(ctypes.byref(d)) == need
     w = _lib.G2KWeights(*([p] * 7))
     rc = lib.g2k_step_grad_f32(ctypes.byref(d), ctypes.byref(w), p, p, p, p, p, None, None, 5e-4,
