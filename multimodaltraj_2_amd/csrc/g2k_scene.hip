@@ -49,8 +49,6 @@ constexpr int kYP = 17;       // train: per-producer dY tile scratch [24][kYP] (
 // train mode
 constexpr int kGFrame = 384;  // per-producer frame scratch: dM [24][8], dcost [8][8], dE [8][16]
 constexpr int kGT_DM = 0, kGT_DC = 192, kGT_DE = 256;
-constexpr int kGTerms = 448;  // one frame's terms (ring slot): dWc_f [24][8], dK1_f [8][10],
-                              // dUaug_f [11][16]
 constexpr int kGAccFixed = 320;   // dWc [24][8], dK1 [8][10], dVe [2][16], dbv [16]
 constexpr int kGA_WC = 0, kGA_K1 = 192, kGA_VE = 272, kGA_BV = 304;
 
@@ -61,7 +59,7 @@ struct SceneLayout {
   // train mode (zero-sized otherwise)
   int wtot;            // window rows of the whole scene ((F - 1) * stride + T)
   int dwo_seq;         // 1: dWo^T accumulated in frame order (one copy); 0: one copy per producer
-  int o_cost, o_gframe, o_gring, o_gacc, o_gdv, o_gdwo, o_gseq;
+  int o_cost, o_gframe, o_gpriv, o_gpdv, o_gacc, o_gdv, o_gdwo, o_gseq;
   int total;           // floats
 };
 
@@ -88,12 +86,13 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_vg = o;    o += rup4((s.wcmax + 3) * kT);       // VG = V @ g: window, Ve0, Ve1, bv rows
   s.wtot = (F > 0 ? F - 1 : 0) * stride + kT;
   s.dwo_seq = (int64_t)NP * Nmax * kT * 4 > 32 * 1024 ? 1 : 0;
-  s.o_cost = s.o_gframe = s.o_gring = s.o_gacc = s.o_gdv = s.o_gdwo = s.o_gseq = o;
+  s.o_cost = s.o_gframe = s.o_gpriv = s.o_gpdv = s.o_gacc = s.o_gdv = s.o_gdwo = s.o_gseq = o;
   if (grad) {
     s.o_cost = o;   o += fc * kT * kT;                 // cost_f per chunk frame (head -> terms)
     s.o_gframe = o; o += NP * kGFrame;
-    s.o_gring = o;  o += fc * kGTerms;                 // the chunk's frame terms, summed at its end
-    s.o_gacc = o;   o += kGAccFixed;
+    s.o_gacc = o;   o += kGAccFixed;                   // (zeroed from here to the seq words)
+    s.o_gpriv = o;  o += NP * kGAccFixed;              // each producer's sums of its frames' terms
+    s.o_gpdv = o;   o += NP * s.wcmax * kD;            // ... and of its dU rows in the chunk
     s.o_gdv = o;    o += rup4(s.wtot * kD);            // dV: window-row gradient [wtot][16]
     s.o_gdwo = o;   o += (s.dwo_seq ? 1 : NP) * Nmax * kT;   // dWo^T [Nmax][8]
     s.o_gseq = o;   o += rup4(2 + (Nmax + 15) / 16);   // chunk count, -, dWo tile seqs
@@ -289,7 +288,7 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
 // Per-workgroup context of the scene kernel (LDS carve-up, scene scalars).
 struct SceneCtx {
   float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sPos, *sVG, *sY;
-  float *sCost, *sGFrame, *sGRing, *sGAcc, *sGdV, *sGdWo;
+  float *sCost, *sGFrame, *sGPriv, *sGPdV, *sGAcc, *sGdV, *sGdWo;
   int* sFlag;     // As ring: global frame + 1 once the frame's As is in its slot
   int* sMflag;    // M ring: global frame + 1 once the frame's M is in its slot
   int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
@@ -709,8 +708,11 @@ __device__ __forceinline__ f32x4 mm16(FA fa, FB fb, int L, int q) {
 }
 
 // GRAD, after the last tile of chunk frame fl: the frame's weight-side
-// terms (one wave, MFMA tiles from LDS) into the chunk's ring slot fl;
-// grad_chunk_sum adds the slots in frame order.
+// terms (one wave, MFMA tiles from LDS) added into this producer's own sums
+// (sGPriv: dWc, dK1, dVe, dbv; sGPdV: the chunk's window rows) — each entry
+// by one lane of one wave, in the producer's frame order: deterministic
+// without any cross-wave ordering; grad_chunk_flush / grad_priv_sum add the
+// producers' sums in producer order.
 //   dcost[u][t] = sum_r Wc[r][u] dM[r][t]          (M = Wc @ cost, :119)
 //   dE[t][d]    = lambda sum_u dcost[t][u] G[d][u] (cost = E @ g, :112-113)
 //   dWc_f[r][u] = sum_t dM[r][t] cost[u][t]
@@ -722,7 +724,8 @@ __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout&
   float* dM = gf + kGT_DM;
   float* dC = gf + kGT_DC;
   float* dE = gf + kGT_DE;
-  float* tm = c.sGRing + fl * kGTerms;
+  float* pacc = c.sGPriv + (c.wv - kRecW) * kGAccFixed;
+  float* pdv = c.sGPdV + (c.wv - kRecW) * lay.wcmax * kD + fl * a.d.stride * kD;
   const int L = c.L, q = c.q, lane = c.lane;
   const float* sm = c.sm;
   const float* cost = c.sCost + fl * kT * kT;
@@ -761,7 +764,7 @@ __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout&
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int r = 16 * h + 4 * q + v;
-          if (r < kL2) tm[r * kT + L] = d[v];
+          if (r < kL2) pacc[kGA_WC + r * kT + L] += d[v];
         }
       }
     }
@@ -774,7 +777,7 @@ __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout&
         [&](int k, int j) { const float x = c.sV[jr * kD + k]; return j < kT + 2 ? x : 0.f; }, L, q);
     if (q < 2 && L < kT + 2) {
 #pragma unroll
-      for (int v = 0; v < 4; ++v) tm[kL2 * kT + (4 * q + v) * 10 + L] = d[v];
+      for (int v = 0; v < 4; ++v) pacc[kGA_K1 + (4 * q + v) * 10 + L] += d[v];
     }
   }
   {                                                       // dUaug_f: [11 j][16 d], K = 8 t
@@ -783,52 +786,52 @@ __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout&
         [&](int k, int j) { return dE[k * kD + j]; }, L, q);
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int j = 4 * q + v;
-      if (j < 11) tm[kL2 * kT + kT * 10 + j * kD + L] = d[v];
+      const int j = 4 * q + v;                              // window rows, Ve0, Ve1, bv
+      if (j < kT) pdv[j * kD + L] += d[v];
+      else if (j < kT + 2) pacc[kGA_VE + (j - kT) * kD + L] += d[v];
+      else if (j == kT + 2) pacc[kGA_BV + L] += d[v];
     }
   }
   wave_lds_sync();                                        // before the next frame's dM
 }
 
-// GRAD, once every producer is done with chunk [fb, fb + cnt): the ring's
-// frame terms added into the scene's accumulators, frame after frame
-// (deterministic), every accumulator entry by one producer lane: dWc, dK1,
-// dVe, dbv, and the window rows the chunk's frames touch (dV[f stride + j]
-// += dU_f[j]).
-__device__ __forceinline__ void grad_chunk_sum(const StepArgs& a, const SceneCtx& c, int fb,
-                                               int cnt, int NP) {
-  const int stride = a.d.stride;
-  const int nfix = kGAccFixed;                              // dWc, dK1, dVe, dbv
-  const int r0 = fb * stride, nrow = (cnt - 1) * stride + kT;   // window rows touched
+// GRAD, once every producer is done with chunk [fb, fb + cnt): the
+// producers' dU rows of the chunk added into the scene's window-row gradient
+// dV in producer order (one entry per producer lane, the chunk's rows), then
+// zeroed for the next chunk.
+__device__ __forceinline__ void grad_chunk_flush(const StepArgs& a, const SceneLayout& lay,
+                                                 const SceneCtx& c, int fb, int cnt, int NP) {
+  const int r0 = fb * a.d.stride, nrow = (cnt - 1) * a.d.stride + kT;
   const int ptid = (c.wv - kRecW) * 64 + c.lane;
-  for (int e = ptid; e < nfix + nrow * kD; e += NP * 64) {
-    // the entry's ring column per frame (-1: the frame does not touch it)
-    int col0 = -1, w = 0;
-    if (e < nfix) {
-      if (e < kGA_VE) col0 = e;                                                // dWc, dK1
-      else if (e < kGA_BV) col0 = kL2 * kT + kT * 10 + kT * kD + (e - kGA_VE);   // dUaug rows 8, 9
-      else col0 = kL2 * kT + kT * 10 + (kT + 2) * kD + (e - kGA_BV);           // dUaug row 10
-    } else {
-      w = (e - nfix) >> 4;                                  // chunk-local window row
-    }
-    const int d = (e - nfix) & 15;
+  const int pitch = lay.wcmax * kD;
+  for (int e = ptid; e < nrow * kD; e += NP * 64) {
+    float v[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) v[p] = p < NP ? c.sGPdV[p * pitch + e] : 0.f;
     float s = 0.f;
-    for (int f0 = 0; f0 < cnt; f0 += 8) {                   // eight frames' loads in flight
-      float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int f = f0 + i;
-        const int j = w - f * stride;
-        const int col = e < nfix ? col0 : kL2 * kT + kT * 10 + (j >= 0 && j < kT ? j : 0) * kD + d;
-        v[i] = c.sGRing[(f < cnt ? f : 0) * kGTerms + col];
-        const bool on = f < cnt && (e < nfix || (j >= 0 && j < kT));
-        v[i] = on ? v[i] : 0.f;
-      }
+    for (int p = 0; p < 16; ++p)
+      if (p < NP) s += v[p];                                 // producer order
+    c.sGdV[r0 * kD + e] += s;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) s += v[i];                 // frame order
-    }
-    if (e < nfix) c.sGAcc[e] += s;
-    else c.sGdV[(r0 + w) * kD + d] += s;
+    for (int p = 0; p < 16; ++p)
+      if (p < NP) c.sGPdV[p * pitch + e] = 0.f;
+  }
+}
+
+// GRAD, after every producer's last frame: sGAcc = the producers' fixed-block
+// sums (dWc, dK1, dVe, dbv) added in producer order.
+__device__ __forceinline__ void grad_priv_sum(const SceneCtx& c, int NP) {
+  const int ptid = (c.wv - kRecW) * 64 + c.lane;
+  for (int e = ptid; e < kGAccFixed; e += NP * 64) {
+    float v[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) v[p] = p < NP ? c.sGPriv[p * kGAccFixed + e] : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p)
+      if (p < NP) s += v[p];
+    c.sGAcc[e] = s;
   }
 }
 
@@ -1002,7 +1005,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) atomicAdd(c.sGseq, 1);
       poll_word(c.sGseq, NP * (fb / lay.fc + 1));
-      if (ntact > 0) grad_chunk_sum(a, c, fb, cnt, NP);   // (no active pedestrian: all zero)
+      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)
     } else {
       for (int k = 0; k < nitems; k += 2) {
         item(k, tgA);
@@ -1048,6 +1051,10 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   // then the scene's gradient row [P + 2] (g2k_weights order) is formed by
   // all producers together
   poll_word(c.sTicket, NP);
+  grad_priv_sum(c, NP);                                // then all producers see sGAcc
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) atomicAdd(c.sGseq + 1, 1);
+  poll_word(c.sGseq + 1, NP);
   const int P = 24 * Nmax + 496;
   float* row = a.grad_rows + (size_t)s * (P + 2);
   const float* ga = c.sGAcc;
@@ -1063,7 +1070,11 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     const int n0 = 16 * t, n = n0 + L;
     f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
     if (n0 < c.nact) {
-      const float* prow = a.pos + (size_t)c.s * a.d.W * Nmax * 2;
+      // one chunk: the whole window is still in LDS (sPos, pitch lay.pp);
+      // else the position rows again from global memory
+      const bool in_lds = lay.fc >= F;
+      const float* prow = in_lds ? c.sPos : a.pos + (size_t)c.s * a.d.W * Nmax * 2;
+      const int pitch = in_lds ? lay.pp : 2 * Nmax;
       const int nks = (lay.wtot + 3) / 4;
       const int nc = n < c.nact ? n : 0;
       // four k-steps' position loads in flight (clamped rows, selected after)
@@ -1073,7 +1084,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int w = 4 * (k0 + i) + q;
-          p[i] = *reinterpret_cast<const float2*>(prow + ((size_t)(w < lay.wtot ? w : 0) * Nmax + nc) * 2);
+          p[i] = *reinterpret_cast<const float2*>(prow + (size_t)(w < lay.wtot ? w : 0) * pitch + 2 * nc);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1154,7 +1165,8 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.sMflag = reinterpret_cast<int*>(smem + lay.o_mflag);
   c.sY = smem + lay.o_y;
   c.sTicket = reinterpret_cast<int*>(c.sRed + 2 * kRB) + kRecW;
-  c.sCost = smem + lay.o_cost; c.sGFrame = smem + lay.o_gframe; c.sGRing = smem + lay.o_gring;
+  c.sCost = smem + lay.o_cost; c.sGFrame = smem + lay.o_gframe;
+  c.sGPriv = smem + lay.o_gpriv; c.sGPdV = smem + lay.o_gpdv;
   c.sGAcc = smem + lay.o_gacc;
   c.sGdV = smem + lay.o_gdv; c.sGdWo = smem + lay.o_gdwo;
   c.sGseq = reinterpret_cast<int*>(smem + lay.o_gseq);
