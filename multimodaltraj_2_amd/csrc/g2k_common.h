@@ -35,6 +35,24 @@ constexpr float kLn2 = 0.6931471805599453f;
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 
+// Range-checked buffer access (raw buffer resource, stride 0): a lane whose
+// byte offset is >= num_records stores nothing / loads zeros.  Per-lane
+// predication without a branch around the memory instruction, so the
+// compiler's vmcnt bookkeeping stays exact (a store under an exec branch
+// makes every later wait conservative: vmcnt(0), i.e. wait for the stores).
+typedef __amdgpu_buffer_rsrc_t brsrc;
+constexpr int kBufOff = 0x7ffffff0;          // an offset no buffer here reaches
+__device__ __forceinline__ brsrc make_brsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void bstore(brsrc r, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+__device__ __forceinline__ float2 bload2(brsrc r, int off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+}
+
 // LDS-DMA: 16 bytes per lane, LDS destination = wave-uniform base + 16*lane.
 __device__ __forceinline__ void dma16(const float* gsrc, float* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,

@@ -562,7 +562,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 __device__ __forceinline__ int mrow(int r) { return (r & 1) * kL + (r >> 1); }
 
 template <bool GRAD>
-__device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, float* pr,
+__device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, brsrc pr,
                                           const float2 (&tg)[4], bool has_t, int Nmax, int nact,
                                           int t, int L, int q, float acc[5], float& lsum,
                                           f32x4 (&dm)[2], f32x4& dWoT) {
@@ -598,11 +598,13 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
       y1 = mfma4(L < kT ? a1[ks] : 0.f, w, y1);            // Y[16 + 4q + v][n] (0 for q >= 2)
     }
   }
-  if (pr && n < nact) {
+  {
+    // range-checked stores (no branch): inactive columns and the block-1
+    // rows of lane groups 2, 3 fall outside the frame's buffer
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      pr[mrow(4 * q + v) * Nmax + n] = y0[v];
-      if (hi) pr[mrow(16 + 4 * q + v) * Nmax + n] = y1[v];
+      bstore(pr, n < nact ? (mrow(4 * q + v) * Nmax + n) * 4 : kBufOff, y0[v]);
+      bstore(pr, (n < nact && hi) ? (mrow(16 + 4 * q + v) * Nmax + n) * 4 : kBufOff, y1[v]);
     }
   }
   // errors: d = Y - target, (x, y) pairs in registers (v = 0, 1 and 2, 3)
@@ -876,19 +878,21 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     }
   };
   // the tile's targets in pred_tile's order: pedestrian 16 t + L, floats
-  // 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row (zero for q >= 2)
+  // 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row (zero for q >= 2),
+  // by range-checked buffer loads of the scene's targets (no branch: items
+  // past the end and lane groups 2, 3 of block 1 read zeros)
+  const brsrc tgr = make_brsrc(a.targets + (size_t)s * F * Nmax * kL2, (uint32_t)F * Nmax * kL2 * 4);
   float2 tgA[4] = {}, tgB[4] = {};
   auto load_item = [&](int fb, int nitems, int k, float2 (&tg)[4]) {
-    if (k >= nitems) return;
+    const bool ok = k < nitems;
     int fl, t;
-    item_ft(k, fl, t);
+    item_ft(ok ? k : 0, fl, t);
     const int ne = 16 * t + L;
-    const int nc = ne < Nmax ? ne : 0;
-    const float2* tp = reinterpret_cast<const float2*>(
-        a.targets + (((size_t)s * F + fb + fl) * Nmax + nc) * kL2);
-    tg[0] = tp[2 * q]; tg[1] = tp[2 * q + 1];
-    tg[2] = tp[8 + 2 * (q & 1)]; tg[3] = tp[9 + 2 * (q & 1)];
-    if (q >= 2) tg[2] = tg[3] = make_float2(0.f, 0.f);
+    const int base = (((fb + fl) * Nmax + (ne < Nmax ? ne : 0)) * kL2) * 4;
+    tg[0] = bload2(tgr, ok ? base + 16 * q : kBufOff);
+    tg[1] = bload2(tgr, ok ? base + 16 * q + 8 : kBufOff);
+    tg[2] = bload2(tgr, ok && q < 2 ? base + 64 + 16 * q : kBufOff);
+    tg[3] = bload2(tgr, ok && q < 2 ? base + 64 + 16 * q + 8 : kBufOff);
   };
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float lsum = 0.f;
@@ -947,7 +951,8 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       item_ft(k, fl, t);
       const int f = fb + fl;
       poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)
-      float* pr = a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : nullptr;
+      const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : a.targets,
+                                  a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
       f32x4 dWoT;
       pred_tile<GRAD>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
                       c.nact, t, L, q, acc, lsum, dm, dWoT);
@@ -977,7 +982,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       auto prefetch = [&](int fi, int t, float2 (&tg)[4]) {
         const int tn = t + 2 < ntact ? t + 2 : (t & 1);
         const int fn = t + 2 < ntact ? fi : fi + 1;
-        if (fn < nfr && tn < ntact) load_item(fb, nitems, fn * ntact + tn, tg);
+        load_item(fb, (fn < nfr && tn < ntact) ? nitems : 0, fn * ntact + tn, tg);
       };
       for (int fi = 0; fi < nfr; ++fi) {
         for (int t = 0; t < ntact; t += 2) {

@@ -4,6 +4,7 @@ copy of multimodaltraj_2_amd/csrc; the copy is built into /tmp and timed on
 the bench workload (HIP events, reference-mode step and train step).
 
 usage: python tools/ab_time.py [CONFIG] [VARIANT ...]   (variants: see VARIANTS)"""
+import ctypes
 import os
 import shutil
 import subprocess
@@ -21,14 +22,21 @@ SCENE = "g2k_scene.hip"
 # diagnostic build: s_memtime stamps (low 32 bits) of scene 0's producer 0 /
 # recurrence wave 0 written past the gradient rows of a widened workspace
 STAMP_DEF = """
-#define G2K_ST(k, cond) do { if ((cond) && c.lane == 0 && a.grad_rows) { \\
+__device__ unsigned g2k_stamp_buf[4096 * 64];
+#define G2K_ST(k, cond) do { if ((cond) && c.lane == 0) { \\
   const unsigned long long _t = __builtin_amdgcn_s_memtime(); \\
-  reinterpret_cast<unsigned*>(a.grad_rows)[(size_t)a.d.S * (24 * a.d.Nmax + 498) + (size_t)c.s * 64 + (k)] \\
-      = (unsigned)_t; } } while (0)
+  g2k_stamp_buf[(size_t)c.s * 64 + (k)] = (unsigned)_t; } } while (0)
+"""
+STAMP_EXPORT = """
+extern "C" int g2k_stamp_copy(unsigned* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2k::g2k_stamp_buf), (size_t)n * 4, 0,
+                                  hipMemcpyDeviceToHost);
+}
 """
 P0 = "c.wv == kRecW"
 STAMPS = [
-    ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", STAMP_DEF + "namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk"),
+    ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
+    ("int scene_step_launch(const StepArgs& a, hipStream_t st) {", "int scene_step_launch(const StepArgs& a, hipStream_t st) {\n  (void)0;"),
     ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
      "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
     ("    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});",
@@ -39,12 +47,19 @@ STAMPS = [
      "        G2K_ST(3 + fi, " + P0 + " && fb == 0 && fi < 5);\n        frame_grad(a, lay, c, pw + fi * NP);\n        G2K_ST(8 + fi, " + P0 + " && fb == 0 && fi < 4);"),
     ("      poll_word(c.sGseq, NP * (fb / lay.fc + 1));",
      "      G2K_ST(24 + pw, fb == 0);\n      poll_word(c.sGseq, NP * (fb / lay.fc + 1));\n      G2K_ST(12, " + P0 + " && fb == 0);"),
-    ("      if (ntact > 0) grad_chunk_sum(a, c, fb, cnt, NP);   // (no active pedestrian: all zero)",
-     "      if (ntact > 0) grad_chunk_sum(a, c, fb, cnt, NP);   // (no active pedestrian: all zero)\n      G2K_ST(13, " + P0 + " && fb == 0);"),
+    ("      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)",
+     "      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)\n      G2K_ST(13, " + P0 + " && fb == 0);"),
     ("  ticket = __builtin_amdgcn_readfirstlane(ticket);", "  ticket = __builtin_amdgcn_readfirstlane(ticket);\n  G2K_ST(14, " + P0 + ");"),
     ("  poll_word(c.sTicket, NP);", "  poll_word(c.sTicket, NP);\n  G2K_ST(15, " + P0 + ");"),
+    ("  poll_word(c.sGseq + 1, NP);", "  poll_word(c.sGseq + 1, NP);\n  G2K_ST(11, " + P0 + ");"),
     ("  // the small blocks and dWo, entry by entry", "  G2K_ST(16, " + P0 + ");\n  // the small blocks and dWo, entry by entry"),
     ("  rc.store(a.h_out", "  G2K_ST(20, c.wv == 0);\n  rc.store(a.h_out"),
+    ("    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
+     "    G2K_ST(21, " + P0 + ");\n    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first\n    G2K_ST(22, " + P0 + ");"),
+    ("    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)",
+     "    G2K_ST(23, " + P0 + ");\n    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)"),
+    ("  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians",
+     "  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians\n  G2K_ST(25, " + P0 + ");"),
     ("    scene_producer<NP, GRAD>(a, lay, c);", "  { G2K_ST(17, " + P0 + "); scene_producer<NP, GRAD>(a, lay, c); }"),
     ("  __syncthreads();                                              // B1: window + weights landed",
      "  G2K_ST(18, " + P0 + " && fb == 0);\n  __syncthreads();\n  G2K_ST(19, " + P0 + " && fb == 0);"),
@@ -64,18 +79,22 @@ TILE = [
     ("        if (lay.dwo_seq) {\n          asm volatile", "        G2K_ST(47, " + P0 + " && t == 0);\n        if (lay.dwo_seq) {\n          asm volatile"),
 ]
 NO_RECUR = [("  const bool live = a.h_in != nullptr;", "  const bool live = false;")]
+NO_RECUR_SCENE = {SCENE: NO_RECUR}
 VARIANTS = {
     "base": {},
-    "no_finalize": {SCENE: [("  poll_word(c.sTicket, NP);\n  const int P = 24 * Nmax + 496;",
-                             "  return;\n  poll_word(c.sTicket, NP);\n  const int P = 24 * Nmax + 496;")]},
+    "no_finalize": {SCENE: [("  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);",
+                             "  return;\n  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);")]},
     "no_frame_grad": {SCENE: [("        frame_grad(a, lay, c, pw + fi * NP);", "")]},
-    "no_tile_grad": {SCENE: [("  if (GRAD) {\n    // the dY entries of other lanes",
-                              "  if (false) {\n    // the dY entries of other lanes")]},
+    "no_tile_grad": {SCENE: [("  if (GRAD) {\n#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      d0[v] = has_t",
+                              "  dWoT = f32x4{0.f, 0.f, 0.f, 0.f};\n  if (false) {\n#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      d0[v] = has_t")]},
     "stamps": {SCENE: STAMPS},
     "stamps_norecur": {SCENE: STAMPS + NO_RECUR},
     "nolsr": {"__flags__": ["-mllvm", "-disable-lsr"]},
+    "no_recur": NO_RECUR_SCENE,
+    "no_pred_store": {SCENE: [("      bstore(pr, n < nact ? (mrow(4 * q + v) * Nmax + n) * 4 : kBufOff, y0[v]);\n      bstore(pr, (n < nact && hi) ? (mrow(16 + 4 * q + v) * Nmax + n) * 4 : kBufOff, y1[v]);", "")]},
     "stamps_nolsr": {SCENE: STAMPS, "__flags__": ["-mllvm", "-disable-lsr"]},
     "stamps_tile": {SCENE: STAMPS + TILE},
+    "stamps_fwd": {SCENE: STAMPS},
 }
 
 
@@ -92,6 +111,8 @@ def build_variant(name):
         for a, b in reps:
             assert a in s, (name, a[:60])
             s = s.replace(a, b)
+        if name.startswith("stamps") and fname == SCENE:
+            s += STAMP_EXPORT
         open(p, "w").write(s)
     out = f"/tmp/libg2k_{name}.so"
     objs = []
@@ -119,31 +140,36 @@ def time_it(fn, reps=200, warm=20):
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
-def stamps(lib, c, t, dev):
+def stamps(lib, c, t, dev, train=True):
     """Run the stamps build once and print scene 0's timeline (cycles)."""
     import ctypes
     import numpy as np
     params = fs.init_params(c["Nmax"], seed=0, device=dev)
-    tp = ts.TrainPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
-    S, P2 = t["pos"].shape[0], ts.grad_size(c["Nmax"]) + 2
-    ws = torch.zeros(S * P2 * 4 + S * 64 * 4, dtype=torch.uint8, device=dev)
-    head = list(tp._head)
-    head[15], head[16] = ws.data_ptr(), ws.numel()
+    if train:
+        plan = ts.TrainPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+    else:
+        plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+    S = t["pos"].shape[0]
     for _ in range(5):
-        rc = lib.g2k_train_step_f32(*head, None, None, 0.0, 0.0, 0.0, tp._stream)
-        assert rc == 0
+        plan.run()
     torch.cuda.synchronize()
-    st = ws[S * P2 * 4:].view(torch.int32).reshape(S, 64).cpu().numpy().astype(np.int64)
+    buf = (ctypes.c_uint * (S * 64))()
+    assert lib.g2k_stamp_copy(buf, S * 64) == 0
+    st = np.frombuffer(buf, dtype=np.uint32).reshape(S, 64).astype(np.int64)
+    print("mode", "train" if train else "forward")
     for sc in (0, S // 2, S - 1):
         r = st[sc]
         rel = (r - r[0]) % (1 << 32)
-        names = {1: "B2", 2: "heads", 3: "tiles f0", 4: "tiles f1", 5: "tiles f2", 8: "fgrad f0",
+        names = {21: "dma issue", 22: "pos dma issued", 23: "segs issued", 25: "nact loaded", 1: "B2",
+                 2: "heads", 3: "tiles f0", 4: "tiles f1", 5: "tiles f2", 8: "fgrad f0",
                  9: "fgrad f1", 10: "fgrad f2", 12: "chunk sync", 13: "chunk sum", 14: "ticket",
-                 15: "ticket=NP", 16: "dWi done", 17: "prod start", 18: "dma waited",
+                 15: "ticket=NP", 11: "priv summed", 16: "dWi done", 17: "prod start", 18: "dma waited",
                  19: "B1", 20: "recur end"}
         print(f"scene {sc} n_active {int(t['n_active'][sc])}: " +
               "  ".join(f"{v}:{rel[k]}" for k, v in names.items() if r[k] != 0))
-        print("   producers' tiles done:", " ".join(str(rel[24 + p]) for p in range(8)))
+        if train:
+            print("   producers' tiles done:", " ".join(str(rel[24 + p]) for p in range(8)),
+                  "(slot 25 collides in train mode)")
         print("   last tile 0 (poll, entry, Y, stores, err, dWoT, dM, dWo):", " ".join(str(rel[k]) for k in (46, 40, 41, 42, 43, 44, 45, 47)))
         print("   heads (start, head done, flags):", " ".join(f"({rel[30 + 3 * i]},{rel[31 + 3 * i]},{rel[32 + 3 * i]})" for i in range(3)))
 
@@ -161,7 +187,8 @@ def main():
         lib = _lib.load(build_variant(name))
         _lib._lib = lib
         if name.startswith("stamps"):
-            stamps(lib, c, t, dev)
+            lib.g2k_stamp_copy.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            stamps(lib, c, t, dev, train=not name.endswith("_fwd"))
             continue
         params = fs.init_params(c["Nmax"], seed=0, device=dev)
         plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
