@@ -561,11 +561,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 //                         accumulated over the frame's tiles in registers)
 __device__ __forceinline__ int mrow(int r) { return (r & 1) * kL + (r >> 1); }
 
-template <bool GRAD>
+// `after_targets` runs once the target registers are consumed (GRAD: the
+// next tile's targets are loaded into them there, before this tile's stores,
+// so the next tile's wait counts exactly those stores).
+template <bool GRAD, typename AfterTargets>
 __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, brsrc pr,
                                           const float2 (&tg)[4], bool has_t, int Nmax, int nact,
                                           int t, int L, int q, float acc[5], float& lsum,
-                                          f32x4 (&dm)[2], f32x4& dWoT) {
+                                          f32x4 (&dm)[2], f32x4& dWoT, AfterTargets after_targets) {
   const int n0 = 16 * t, n = n0 + L;
   const bool hi = q < 2;                                   // block-1 rows exist (r < 24)
   f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
@@ -598,6 +601,16 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
       y1 = mfma4(L < kT ? a1[ks] : 0.f, w, y1);            // Y[16 + 4q + v][n] (0 for q >= 2)
     }
   }
+  // errors: d = Y - target, (x, y) pairs in registers (v = 0, 1 and 2, 3)
+  float d0[4], d1[4];
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    d0[2 * v] = y0[2 * v] - tg[v].x;       d0[2 * v + 1] = y0[2 * v + 1] - tg[v].y;
+    d1[2 * v] = hi ? y1[2 * v] - tg[2 + v].x : 0.f;
+    d1[2 * v + 1] = hi ? y1[2 * v + 1] - tg[2 + v].y : 0.f;
+  }
+  after_targets();
+  asm volatile("" ::: "memory");                           // ... then the stores
   {
     // range-checked stores (no branch): inactive columns and the block-1
     // rows of lane groups 2, 3 fall outside the frame's buffer
@@ -606,14 +619,6 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
       bstore(pr, n < nact ? (mrow(4 * q + v) * Nmax + n) * 4 : kBufOff, y0[v]);
       bstore(pr, (n < nact && hi) ? (mrow(16 + 4 * q + v) * Nmax + n) * 4 : kBufOff, y1[v]);
     }
-  }
-  // errors: d = Y - target, (x, y) pairs in registers (v = 0, 1 and 2, 3)
-  float d0[4], d1[4];
-#pragma unroll
-  for (int v = 0; v < 2; ++v) {
-    d0[2 * v] = y0[2 * v] - tg[v].x;       d0[2 * v + 1] = y0[2 * v + 1] - tg[v].y;
-    d1[2 * v] = hi ? y1[2 * v] - tg[2 + v].x : 0.f;
-    d1[2 * v + 1] = hi ? y1[2 * v + 1] - tg[2 + v].y : 0.f;
   }
   float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f;
 #pragma unroll
@@ -908,8 +913,19 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     } else {
       nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;
     }
-    load_item(fb, nitems, 0, tgA);    // first tiles' targets: in flight during the heads
-    load_item(fb, nitems, 1, tgB);
+    // the first tiles' targets: in flight during the heads.  GRAD: one
+    // buffer, then eight dummy stores (out of range) so that every wait on a
+    // target load in the tile loop has the same eight younger stores before
+    // it and the compiler's counts stay exact (vmcnt(8), not vmcnt(0))
+    load_item(fb, nitems, 0, tgA);
+    if (GRAD) {
+      asm volatile("" ::: "memory");
+      const brsrc none = make_brsrc(a.targets, 0u);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bstore(none, kBufOff, 0.f);
+    } else {
+      load_item(fb, nitems, 1, tgB);
+    }
     // Rm = Wr @ Rel, Rel = Ve * Ve (train.py:194-195, g2k_lstm_mcr.py:106):
     // rows t = 4q + i of column L, zero for t >= 8
     float rm[4];
@@ -946,7 +962,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     }
     // phase 2 — predictions and errors (GRAD: and the gradient)
     float* ys = c.sY + pw * kL2 * kYP;
-    auto item = [&](int k, const float2 (&tg)[4]) {
+    auto item = [&](int k, float2 (&tg)[4], auto after_targets) {
       int fl, t;
       item_ft(k, fl, t);
       const int f = fb + fl;
@@ -955,7 +971,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
                                   a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
       f32x4 dWoT;
       pred_tile<GRAD>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
-                      c.nact, t, L, q, acc, lsum, dm, dWoT);
+                      c.nact, t, L, q, acc, lsum, dm, dWoT, after_targets);
       if (GRAD) {
         // dWo^T[n0 + 4q + v][t = L]: one copy per producer, or one copy
         // added to in frame order (tile sequence word) when that is too big
@@ -974,24 +990,15 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       }
     };
     if (GRAD) {
-      // frame by frame: tiles in pairs (even tiles in buffer A, odd in B),
-      // each buffer prefetching its next tile of the same parity — in this
-      // frame, else tile 0 (A) / 1 (B) of this producer's next frame — and
-      // the frame's weight-side terms after its last tile (one call site)
+      // frame by frame, tile by tile, one target buffer: each tile loads the
+      // next tile's targets (this frame's next tile, else the next frame's
+      // first) as soon as its own are consumed, then stores its predictions
       const int nfr = nitems / (ntact > 0 ? ntact : 1);
-      auto prefetch = [&](int fi, int t, float2 (&tg)[4]) {
-        const int tn = t + 2 < ntact ? t + 2 : (t & 1);
-        const int fn = t + 2 < ntact ? fi : fi + 1;
-        load_item(fb, (fn < nfr && tn < ntact) ? nitems : 0, fn * ntact + tn, tg);
-      };
+      float2 (&tg)[4] = tgA;
       for (int fi = 0; fi < nfr; ++fi) {
-        for (int t = 0; t < ntact; t += 2) {
-          item(fi * ntact + t, tgA);
-          prefetch(fi, t, tgA);
-          if (t + 1 < ntact) {
-            item(fi * ntact + t + 1, tgB);
-            prefetch(fi, t + 1, tgB);
-          }
+        for (int t = 0; t < ntact; ++t) {
+          const int k = fi * ntact + t;
+          item(k, tg, [&] { load_item(fb, nitems, k + 1, tg); });
         }
         // the frame's dM to this wave's scratch (M's physical rows), then its terms
         if (L < kT) {
@@ -1013,10 +1020,10 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)
     } else {
       for (int k = 0; k < nitems; k += 2) {
-        item(k, tgA);
+        item(k, tgA, [] {});
         load_item(fb, nitems, k + 2, tgA);
         if (k + 1 < nitems) {
-          item(k + 1, tgB);
+          item(k + 1, tgB, [] {});
           load_item(fb, nitems, k + 3, tgB);
         }
       }
