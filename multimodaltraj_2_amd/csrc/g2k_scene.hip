@@ -47,8 +47,8 @@ constexpr int kSceneSmall = 1088;
 constexpr int kKA = 12;       // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
 constexpr int kYP = 17;       // train: per-producer dY tile scratch [24][kYP] (pitch: bank spread)
 // train mode
-constexpr int kGFrame = 384;  // per-producer frame scratch: dM [24][8], dcost [8][8], dE [8][16]
-constexpr int kGT_DM = 0, kGT_DC = 192, kGT_DE = 256;
+constexpr int kGFrame = 192;  // per-producer frame scratch: dM [24][8] (frame_grad's P6)
+constexpr int kGT_DM = 0;
 constexpr int kGAccFixed = 320;   // dWc [24][8], dK1 [8][10], dVe [2][16], dbv [16]
 constexpr int kGA_WC = 0, kGA_K1 = 192, kGA_VE = 272, kGA_BV = 304;
 
@@ -726,78 +726,104 @@ __device__ __forceinline__ f32x4 mm16(FA fa, FB fb, int L, int q) {
 //   dK1_f[t][j] = sum_d dE[t][d] Uaug[j][d]        (E = K1 @ Uaug, j < 10)
 //   dUaug_f[j][d] = sum_t K1[t][j] dE[t][d]        (j < 8: window rows, 8-9: Ve, 10: bv)
 __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout& lay,
-                                           const SceneCtx& c, int fl) {
-  float* gf = c.sGFrame + (c.wv - kRecW) * kGFrame;
-  float* dM = gf + kGT_DM;
-  float* dC = gf + kGT_DC;
-  float* dE = gf + kGT_DE;
+                                           const SceneCtx& c, int fl, const f32x4 (&dm)[2]) {
+  // The products chain through the MFMA registers: a result D (lane (L, q)
+  // reg v = D[4q+v][L]) is the next product's B operand as is (k = 4q + ks
+  // <-> reg ks) or its A operand transposed (A[L][4q+ks] = D[4q+ks][L]), so
+  // only the constant operands and dWc's dM come from LDS.
+  //   P1 dcost^T[t2][t1] = sum_r dM[r][t2] Wc[r][t1]      (A: dm registers,
+  //                                                         rows r interleaved)
+  //   P2 dE[t1][d]   = lambda sum_t2 dcost[t1][t2] G[d][t2]   (A: P1^T)
+  //   P3 dE^T[d][t1] = lambda sum_t2 G[d][t2] dcost^T[t2][t1] (B: P1)
+  //   P4 dU[j][d]    = sum_t1 K1[t1][j] dE[t1][d]          (B: P2)
+  //   P5 dK1[t1][j]  = sum_d dE[t1][d] Uaug[j][d]          (A: P3^T)
+  //   P6 dWc[r][t1]  = sum_t2 dM[r][t2] cost[t1][t2]       (dM from LDS)
+  const float* dM = c.sGFrame + (c.wv - kRecW) * kGFrame + kGT_DM;
   float* pacc = c.sGPriv + (c.wv - kRecW) * kGAccFixed;
   float* pdv = c.sGPdV + (c.wv - kRecW) * lay.wcmax * kD + fl * a.d.stride * kD;
-  const int L = c.L, q = c.q, lane = c.lane;
+  const int L = c.L, q = c.q, L7 = L & 7, q1 = q & 1;
   const float* sm = c.sm;
   const float* cost = c.sCost + fl * kT * kT;
   const int wrow0 = fl * a.d.stride;
-  wave_lds_sync();                                        // the frame's dM, all tiles added
-  {                                                       // dcost: [8 u][8 t], K = 24 rows r
-    const f32x4 d = mm16<6>(
-        [&](int i, int k) { const float x = sm[SM_WC + k * kT + (i & 7)]; return i < kT ? x : 0.f; },
-        [&](int k, int j) { const float x = dM[k * kT + (j & 7)]; return j < kT ? x : 0.f; }, L, q);
-    if (q < 2 && L < kT) {
+  const int jr = L < kT ? wrow0 + L : lay.wcmax + (L < kT + 2 ? L - kT : 1);   // Uaug row j = L
+  // every operand load first (clamped addresses), selects after
+  float wc[8], gq[4], k1[4], ua[4], mA[4], cB[2];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) dC[(4 * q + v) * kT + L] = d[v];
-    }
+  for (int ks = 0; ks < 4; ++ks) {
+    // dm's rows r are in the tiles' interleaved order: Wc row mrow(r)
+    wc[ks] = sm[SM_WC + mrow(4 * q + ks) * kT + L7];              // Wc[r = 4q+ks][t1 = L]
+    wc[4 + ks] = sm[SM_WC + mrow(16 + 4 * q1 + ks) * kT + L7];    // Wc[16 + 4q+ks][t1]
+    gq[ks] = sm[SM_G + L * kT + 4 * q1 + ks];                     // G[d = L][t2 = 4q+ks]
+    k1[ks] = sm[SM_K1 + (4 * q1 + ks) * kKA + (L < kKA ? L : 0)]; // K1[t1 = 4q+ks][j = L]
+    ua[ks] = c.sV[jr * kD + 4 * q + ks];                          // Uaug[j = L][d = 4q+ks]
   }
-  wave_lds_sync();
-  {                                                       // dE: [8 t][16 d], K = 8 u
-    const f32x4 d = mm16<2>(
-        [&](int i, int k) { const float x = dC[(i & 7) * kT + k]; return i < kT ? x : 0.f; },
-        [&](int k, int j) { return sm[SM_G + j * kT + k]; }, L, q);
-    if (q < 2) {
+  wave_lds_sync();                                        // the frame's dM in LDS (P6)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) dE[(4 * q + v) * kD + L] = a.lambda * d[v];
-    }
+  for (int ks = 0; ks < 2; ++ks) {
+    const int t2 = 4 * ks + q;
+    mA[2 * ks] = dM[L * kT + (t2 & 7)];                           // dM[r = L][t2]
+    mA[2 * ks + 1] = dM[(16 + L7) * kT + (t2 & 7)];               // dM[16 + L][t2]
+    cB[ks] = cost[L7 * kT + (t2 & 7)];                            // cost[t1 = L][t2]
   }
-  {                                                       // dWc_f: [24 r][8 u], K = 8 t
+  asm volatile("" : "+v"(wc[0]), "+v"(wc[1]), "+v"(wc[2]), "+v"(wc[3]), "+v"(wc[4]), "+v"(wc[5]),
+               "+v"(wc[6]), "+v"(wc[7]), "+v"(gq[0]), "+v"(gq[1]), "+v"(gq[2]), "+v"(gq[3]));
+  asm volatile("" : "+v"(k1[0]), "+v"(k1[1]), "+v"(k1[2]), "+v"(k1[3]), "+v"(ua[0]), "+v"(ua[1]),
+               "+v"(ua[2]), "+v"(ua[3]), "+v"(mA[0]), "+v"(mA[1]), "+v"(mA[2]), "+v"(mA[3]),
+               "+v"(cB[0]), "+v"(cB[1]));
+  const bool lo = q < 2;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4 d = mm16<2>(
-          [&](int i, int k) {
-            const int r = 16 * h + i;
-            const float x = dM[(r < kL2 ? r : 0) * kT + k];
-            return r < kL2 ? x : 0.f;
-          },
-          [&](int k, int j) { const float x = cost[(j & 7) * kT + k]; return j < kT ? x : 0.f; }, L, q);
-      if (L < kT) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int r = 16 * h + 4 * q + v;
-          if (r < kL2) pacc[kGA_WC + r * kT + L] += d[v];
-        }
-      }
-    }
+  for (int ks = 0; ks < 4; ++ks) {
+    wc[4 + ks] = lo ? wc[4 + ks] : 0.f;                           // rows r >= 24
+    gq[ks] = lo ? a.lambda * gq[ks] : 0.f;                        // t2 >= 8
+    k1[ks] = (lo && L < kT + 3) ? k1[ks] : 0.f;                   // t1 >= 8, j >= 11
+    ua[ks] = L < kT + 2 ? ua[ks] : 0.f;                           // j >= 10
   }
-  wave_lds_sync();                                        // dE complete
-  {                                                       // dK1_f: [8 t][10 j], K = 16 d
-    const int jr = L < kT ? wrow0 + L : lay.wcmax + (L < kT + 2 ? L - kT : 1);   // Uaug row j = L
-    const f32x4 d = mm16<4>(
-        [&](int i, int k) { const float x = dE[(i & 7) * kD + k]; return i < kT ? x : 0.f; },
-        [&](int k, int j) { const float x = c.sV[jr * kD + k]; return j < kT + 2 ? x : 0.f; }, L, q);
-    if (q < 2 && L < kT + 2) {
+  // P1
+  f32x4 dcT = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int v = 0; v < 4; ++v) pacc[kGA_K1 + (4 * q + v) * 10 + L] += d[v];
-    }
+  for (int ks = 0; ks < 4; ++ks) dcT = mfma4(dm[0][ks], wc[ks], dcT);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) dcT = mfma4(dm[1][ks], wc[4 + ks], dcT);
+  // P6 (independent of P1..P5)
+  f32x4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const float cb = L < kT ? cB[ks] : 0.f;
+    w0 = mfma4(mA[2 * ks], cb, w0);                               // dWc[4q+v][t1 = L]
+    w1 = mfma4(L < kT ? mA[2 * ks + 1] : 0.f, cb, w1);            // dWc[16 + 4q+v][t1]
   }
-  {                                                       // dUaug_f: [11 j][16 d], K = 8 t
-    const f32x4 d = mm16<2>(
-        [&](int i, int k) { const float x = sm[SM_K1 + k * kKA + (i < kKA ? i : 0)]; return i < 11 ? x : 0.f; },
-        [&](int k, int j) { return dE[k * kD + j]; }, L, q);
+  // P2, P3
+  f32x4 dE = {0.f, 0.f, 0.f, 0.f}, dET = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    dE = mfma4(dcT[ks], gq[ks], dE);
+    dET = mfma4(gq[ks], dcT[ks], dET);
+  }
+  // P4, P5
+  f32x4 dU = {0.f, 0.f, 0.f, 0.f}, dK = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    dU = mfma4(k1[ks], lo ? dE[ks] : 0.f, dU);
+    dK = mfma4(dET[ks], ua[ks], dK);
+  }
+  // into this producer's sums
+  if (L < kT) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int j = 4 * q + v;                              // window rows, Ve0, Ve1, bv
-      if (j < kT) pdv[j * kD + L] += d[v];
-      else if (j < kT + 2) pacc[kGA_VE + (j - kT) * kD + L] += d[v];
-      else if (j == kT + 2) pacc[kGA_BV + L] += d[v];
+      pacc[kGA_WC + (4 * q + v) * kT + L] += w0[v];
+      if (lo) pacc[kGA_WC + (16 + 4 * q + v) * kT + L] += w1[v];
     }
+  }
+  if (lo && L < kT + 2) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) pacc[kGA_K1 + (4 * q + v) * 10 + L] += dK[v];
+  }
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int j = 4 * q + v;                              // window rows, Ve0, Ve1, bv
+    if (j < kT) pdv[j * kD + L] += dU[v];
+    else if (j < kT + 2) pacc[kGA_VE + (j - kT) * kD + L] += dU[v];
+    else if (j == kT + 2) pacc[kGA_BV + L] += dU[v];
   }
   wave_lds_sync();                                        // before the next frame's dM
 }
@@ -1009,9 +1035,9 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
             if (q < 2) dMs[mrow(16 + 4 * q + v) * kT + L] = dm[1][v];
           }
         }
+        frame_grad(a, lay, c, pw + fi * NP, dm);
         dm[0] = f32x4{0.f, 0.f, 0.f, 0.f};
         dm[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        frame_grad(a, lay, c, pw + fi * NP);
       }
       // every producer done with the chunk's frames -> add the ring
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
