@@ -75,8 +75,9 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
-  s.o_y = o;     o += grad ? NP * kL2 * kYP : 0;      // dY tile scratch (train)
-  s.o_met = o;   o += NP * 8;
+  const int NG = NP + kRecW;                          // train: producers + recurrence waves
+  s.o_y = o;     o += grad ? NG * kL2 * kYP : 0;      // dY tile scratch (train)
+  s.o_met = o;   o += (grad ? NG : NP) * 8;
   s.o_ring = o;  o += fc * kD * kD;
   s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
   s.o_flag = o;  o += rup4(fc);                      // As ring flags (recurrence polls)
@@ -85,16 +86,16 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_pos = o;   o += s.wcmax * s.pp;                  // raw position window (LDS-DMA)
   s.o_vg = o;    o += rup4((s.wcmax + 3) * kT);       // VG = V @ g: window, Ve0, Ve1, bv rows
   s.wtot = (F > 0 ? F - 1 : 0) * stride + kT;
-  s.dwo_seq = (int64_t)NP * Nmax * kT * 4 > 32 * 1024 ? 1 : 0;
+  s.dwo_seq = (int64_t)(NP + kRecW) * Nmax * kT * 4 > 32 * 1024 ? 1 : 0;
   s.o_cost = s.o_gframe = s.o_gpriv = s.o_gpdv = s.o_gacc = s.o_gdv = s.o_gdwo = s.o_gseq = o;
   if (grad) {
     s.o_cost = o;   o += fc * kT * kT;                 // cost_f per chunk frame (head -> terms)
-    s.o_gframe = o; o += NP * kGFrame;
+    s.o_gframe = o; o += NG * kGFrame;
     s.o_gacc = o;   o += kGAccFixed;                   // (zeroed from here to the seq words)
-    s.o_gpriv = o;  o += NP * kGAccFixed;              // each producer's sums of its frames' terms
-    s.o_gpdv = o;   o += NP * s.wcmax * kD;            // ... and of its dU rows in the chunk
+    s.o_gpriv = o;  o += NG * kGAccFixed;              // each worker's sums of its frames' terms
+    s.o_gpdv = o;   o += NG * s.wcmax * kD;            // ... and of its dU rows in the chunk
     s.o_gdv = o;    o += rup4(s.wtot * kD);            // dV: window-row gradient [wtot][16]
-    s.o_gdwo = o;   o += (s.dwo_seq ? 1 : NP) * Nmax * kT;   // dWo^T [Nmax][8]
+    s.o_gdwo = o;   o += (s.dwo_seq ? 1 : NG) * Nmax * kT;   // dWo^T [Nmax][8]
     s.o_gseq = o;   o += rup4(2 + (Nmax + 15) / 16);   // chunk count, -, dWo tile seqs
   }
   s.total = o;
@@ -726,7 +727,8 @@ __device__ __forceinline__ f32x4 mm16(FA fa, FB fb, int L, int q) {
 //   dK1_f[t][j] = sum_d dE[t][d] Uaug[j][d]        (E = K1 @ Uaug, j < 10)
 //   dUaug_f[j][d] = sum_t K1[t][j] dE[t][d]        (j < 8: window rows, 8-9: Ve, 10: bv)
 __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout& lay,
-                                           const SceneCtx& c, int fl, const f32x4 (&dm)[2]) {
+                                           const SceneCtx& c, int fl, const f32x4 (&dm)[2],
+                                           int slot) {
   // The products chain through the MFMA registers: a result D (lane (L, q)
   // reg v = D[4q+v][L]) is the next product's B operand as is (k = 4q + ks
   // <-> reg ks) or its A operand transposed (A[L][4q+ks] = D[4q+ks][L]), so
@@ -738,9 +740,9 @@ __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout&
   //   P4 dU[j][d]    = sum_t1 K1[t1][j] dE[t1][d]          (B: P2)
   //   P5 dK1[t1][j]  = sum_d dE[t1][d] Uaug[j][d]          (A: P3^T)
   //   P6 dWc[r][t1]  = sum_t2 dM[r][t2] cost[t1][t2]       (dM from LDS)
-  const float* dM = c.sGFrame + (c.wv - kRecW) * kGFrame + kGT_DM;
-  float* pacc = c.sGPriv + (c.wv - kRecW) * kGAccFixed;
-  float* pdv = c.sGPdV + (c.wv - kRecW) * lay.wcmax * kD + fl * a.d.stride * kD;
+  const float* dM = c.sGFrame + slot * kGFrame + kGT_DM;
+  float* pacc = c.sGPriv + slot * kGAccFixed;
+  float* pdv = c.sGPdV + slot * lay.wcmax * kD + fl * a.d.stride * kD;
   const int L = c.L, q = c.q, L7 = L & 7, q1 = q & 1;
   const float* sm = c.sm;
   const float* cost = c.sCost + fl * kT * kT;
@@ -834,37 +836,191 @@ __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout&
 // zeroed for the next chunk.
 __device__ __forceinline__ void grad_chunk_flush(const StepArgs& a, const SceneLayout& lay,
                                                  const SceneCtx& c, int fb, int cnt, int NP) {
+  const int NG = NP + kRecW;
   const int r0 = fb * a.d.stride, nrow = (cnt - 1) * a.d.stride + kT;
   const int ptid = (c.wv - kRecW) * 64 + c.lane;
   const int pitch = lay.wcmax * kD;
   for (int e = ptid; e < nrow * kD; e += NP * 64) {
     float v[16];
 #pragma unroll
-    for (int p = 0; p < 16; ++p) v[p] = p < NP ? c.sGPdV[p * pitch + e] : 0.f;
+    for (int p = 0; p < 16; ++p) v[p] = p < NG ? c.sGPdV[p * pitch + e] : 0.f;
     float s = 0.f;
 #pragma unroll
     for (int p = 0; p < 16; ++p)
-      if (p < NP) s += v[p];                                 // producer order
+      if (p < NG) s += v[p];                                 // worker order
     c.sGdV[r0 * kD + e] += s;
 #pragma unroll
     for (int p = 0; p < 16; ++p)
-      if (p < NP) c.sGPdV[p * pitch + e] = 0.f;
+      if (p < NG) c.sGPdV[p * pitch + e] = 0.f;
   }
 }
 
 // GRAD, after every producer's last frame: sGAcc = the producers' fixed-block
 // sums (dWc, dK1, dVe, dbv) added in producer order.
 __device__ __forceinline__ void grad_priv_sum(const SceneCtx& c, int NP) {
+  const int NG = NP + kRecW;
   const int ptid = (c.wv - kRecW) * 64 + c.lane;
   for (int e = ptid; e < kGAccFixed; e += NP * 64) {
     float v[16];
 #pragma unroll
-    for (int p = 0; p < 16; ++p) v[p] = p < NP ? c.sGPriv[p * kGAccFixed + e] : 0.f;
+    for (int p = 0; p < 16; ++p) v[p] = p < NG ? c.sGPriv[p * kGAccFixed + e] : 0.f;
     float s = 0.f;
 #pragma unroll
     for (int p = 0; p < 16; ++p)
-      if (p < NP) s += v[p];
+      if (p < NG) s += v[p];
     c.sGAcc[e] = s;
+  }
+}
+
+// Pedestrian n = 16 t + L has targets (n < n_active and its ped_mask byte
+// set): bit t of the lane's word.  Read once per wave (a mask load inside the
+// tile loop would make the compiler wait for the targets prefetched behind it).
+__device__ __forceinline__ unsigned scene_act_bits(const StepArgs& a, const SceneCtx& c) {
+  const int Nmax = a.d.Nmax;
+  const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)c.s * Nmax : nullptr;
+  bool on[kMaxN / 64];
+#pragma unroll
+  for (int j = 0; j < kMaxN / 64; ++j) {
+    const int n = c.lane + 64 * j;
+    on[j] = n < c.nact && (pm ? pm[n < Nmax ? n : 0] != 0 : true);
+  }
+  unsigned bits = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxN / 64; ++j) {
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(on[j]);
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) bits |= (unsigned)((b >> (16 * tt + c.L)) & 1ull) << (4 * j + tt);
+  }
+  return bits;
+}
+
+// Train mode: the last R frames of the scene's last chunk go to the
+// recurrence waves (one each, after their recurrence), so the producers'
+// share shrinks when they have at least two frames each.
+__device__ __forceinline__ int grad_rec_frames(int cnt, int NP) { return cnt >= 2 * NP ? kRecW : 0; }
+
+// The targets of tile t of chunk frame fl in pred_tile's order (pedestrian
+// 16 t + L, floats 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row, zero
+// for q >= 2) by range-checked buffer loads (no branch: !ok reads zeros).
+__device__ __forceinline__ void load_targets(brsrc tgr, int Nmax, int fb, int fl, int t, bool ok,
+                                             int L, int q, float2 (&tg)[4]) {
+  const int ne = 16 * t + L;
+  const int base = (((fb + fl) * Nmax + (ne < Nmax ? ne : 0)) * kL2) * 4;
+  tg[0] = bload2(tgr, ok ? base + 16 * q : kBufOff);
+  tg[1] = bload2(tgr, ok ? base + 16 * q + 8 : kBufOff);
+  tg[2] = bload2(tgr, ok && q < 2 ? base + 64 + 16 * q : kBufOff);
+  tg[3] = bload2(tgr, ok && q < 2 ? base + 64 + 16 * q + 8 : kBufOff);
+}
+
+__device__ __forceinline__ brsrc scene_targets_rsrc(const StepArgs& a, int s) {
+  return make_brsrc(a.targets + (size_t)s * a.d.F * a.d.Nmax * kL2,
+                    (uint32_t)a.d.F * a.d.Nmax * kL2 * 4);
+}
+
+// Eight out-of-range stores right after the first target load of a tile loop:
+// every wait on a target load in the loop then has the same eight younger
+// stores before it and the compiler's counts stay exact (vmcnt(8), not 0).
+__device__ __forceinline__ void balance_stores(const StepArgs& a) {
+  asm volatile("" ::: "memory");
+  const brsrc none = make_brsrc(a.targets, 0u);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bstore(none, kBufOff, 0.f);
+}
+
+// GRAD: one gradient worker's frames fl = f0, f0 + fstep, ... < fend of the
+// chunk at fb (worker `slot`: producer pw = slot, recurrence wave NP + w):
+// per tile the predictions, the a9 terms, dY, dWo^T (into the worker's copy,
+// or in frame order when one copy is kept), dM in registers; per frame the
+// weight-side terms (frame_grad) into the worker's sums.  One target buffer:
+// each tile loads the next tile's targets as soon as its own are consumed,
+// before its prediction stores (tg holds the first tile's targets on entry
+// when `preloaded`).
+__device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout& lay,
+                                            const SceneCtx& c, int slot, int fb, int f0, int fstep,
+                                            int fend, unsigned act_bits, float (&acc)[5],
+                                            float& lsum, float2 (&tg)[4], bool preloaded) {
+  const int Nmax = a.d.Nmax, F = a.d.F, L = c.L, q = c.q, ntact = c.ntact;
+  const brsrc tgr = scene_targets_rsrc(a, c.s);
+  if (!preloaded) {
+    load_targets(tgr, Nmax, fb, f0, 0, f0 < fend, L, q, tg);
+    balance_stores(a);
+  }
+  float* ys = c.sY + slot * kL2 * kYP;
+  f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int fl = f0; fl < fend; fl += fstep) {
+    const int f = fb + fl;
+    poll_flag(c.sMflag + fl, f + 1);                     // M of this frame (a producer's head)
+    const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)c.s * F + f) * kL2 * Nmax : a.targets,
+                                a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
+    for (int t = 0; t < ntact; ++t) {
+      const bool nxt = t + 1 < ntact;                    // the next tile: this frame's, else the next frame's
+      const int nfl = nxt ? fl : fl + fstep, nt = nxt ? t + 1 : 0;
+      f32x4 dWoT;
+      pred_tile<true>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
+                      c.nact, t, L, q, acc, lsum, dm, dWoT,
+                      [&] { load_targets(tgr, Nmax, fb, nfl, nt, nfl < fend, L, q, tg); });
+      // dWo^T[n0 + 4q + v][t = L]: one copy per worker, or one copy added
+      // to in frame order (tile sequence word) when that is too big
+      const int nb = 16 * t + 4 * q;
+      float* dst = c.sGdWo + (lay.dwo_seq ? 0 : slot * Nmax * kT);
+      if (lay.dwo_seq) poll_word(c.sGseq + 2 + t, f);
+      if (L < kT) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (nb + v < Nmax) dst[(nb + v) * kT + L] += dWoT[v];
+      }
+      if (lay.dwo_seq) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (c.lane == 0) lds_store_flag(c.sGseq + 2 + t, f + 1);
+      }
+    }
+    // the frame's dM to this worker's scratch (M's physical rows), then its terms
+    if (L < kT) {
+      float* dMs = c.sGFrame + slot * kGFrame + kGT_DM;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        dMs[mrow(4 * q + v) * kT + L] = dm[0][v];
+        if (q < 2) dMs[mrow(16 + 4 * q + v) * kT + L] = dm[1][v];
+      }
+    }
+    frame_grad(a, lay, c, fl, dm, slot);
+    dm[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dm[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// Metrics (and the train loss): each worker publishes its partial sums in
+// its row of sMet, then takes a ticket (LDS atomic); the wave drawing the
+// last of `nrows` tickets sums the rows in worker order (deterministic) and
+// writes the scene's metrics row.
+__device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCtx& c, int row,
+                                                int nrows, const float (&acc)[5], float lsum,
+                                                bool grad) {
+  const int lane = c.lane;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const float v = wave_sum(acc[k]);
+    if (lane == 0) c.sMet[row * 8 + k] = v;
+  }
+  if (grad) {
+    const float v = wave_sum(lsum);
+    if (lane == 0) c.sMet[row * 8 + 5] = v;
+  }
+  int ticket = 0;
+  if (lane == 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // partials before the ticket
+    ticket = atomicAdd(c.sTicket, 1);
+  }
+  ticket = __builtin_amdgcn_readfirstlane(ticket);
+  if (ticket == nrows - 1 && lane < 8 && a.metrics) {
+    float v = 0.f;
+    if (lane < 5) {
+      if (c.nf > 0)
+        for (int p = 0; p < nrows; ++p) v += c.sMet[p * 8 + lane];
+    } else if (lane == 5) {
+      v = (float)c.nf;
+    }
+    a.metrics[(size_t)c.s * 8 + lane] = v;
   }
 }
 
@@ -874,82 +1030,41 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
   const int pw = c.wv - kRecW, L = c.L, q = c.q, lane = c.lane, s = c.s, ntact = c.ntact;
-  // pedestrian n = 16 t + L has targets (n < n_active and its
-  // ped_mask byte set): bit t of this lane's act_bits.  Read once, before the
-  // first staging wait (a mask load inside the tile loop would make the
-  // compiler wait for the targets prefetched behind it)
-  unsigned act_bits = 0;
-  {
-    const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)s * Nmax : nullptr;
-    bool on[kMaxN / 64];
-#pragma unroll
-    for (int j = 0; j < kMaxN / 64; ++j) {
-      const int n = lane + 64 * j;
-      on[j] = n < c.nact && (pm ? pm[n < Nmax ? n : 0] != 0 : true);
-    }
-#pragma unroll
-    for (int j = 0; j < kMaxN / 64; ++j) {
-      const unsigned long long b = __builtin_amdgcn_ballot_w64(on[j]);
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) act_bits |= (unsigned)((b >> (16 * tt + L)) & 1ull) << (4 * j + tt);
-    }
-  }
-  // tile items of a chunk.  Forward: item j -> frame j / ntact, tile
-  // j % ntact; this producer takes items pw, pw + NP, ...  GRAD: this
-  // producer owns whole frames pw, pw + NP, ... (its k-th item is tile
-  // k % ntact of its (k / ntact)-th frame)
+  const unsigned act_bits = scene_act_bits(a, c);
+  // tile items of a chunk (forward): item j -> frame j / ntact, tile
+  // j % ntact; this producer takes items pw, pw + NP, ...  (GRAD: whole
+  // frames per worker, grad_frames)
   auto item_ft = [&](int k, int& fl, int& t) {
-    if (GRAD) {
-      fl = pw + (k / ntact) * NP;
-      t = k - (k / ntact) * ntact;
-    } else {
-      const int j = pw + k * NP;
-      fl = j / ntact;
-      t = j - fl * ntact;
-    }
+    const int j = pw + k * NP;
+    fl = j / ntact;
+    t = j - fl * ntact;
   };
-  // the tile's targets in pred_tile's order: pedestrian 16 t + L, floats
-  // 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row (zero for q >= 2),
-  // by range-checked buffer loads of the scene's targets (no branch: items
-  // past the end and lane groups 2, 3 of block 1 read zeros)
-  const brsrc tgr = make_brsrc(a.targets + (size_t)s * F * Nmax * kL2, (uint32_t)F * Nmax * kL2 * 4);
+  const brsrc tgr = scene_targets_rsrc(a, s);
   float2 tgA[4] = {}, tgB[4] = {};
   auto load_item = [&](int fb, int nitems, int k, float2 (&tg)[4]) {
     const bool ok = k < nitems;
     int fl, t;
     item_ft(ok ? k : 0, fl, t);
-    const int ne = 16 * t + L;
-    const int base = (((fb + fl) * Nmax + (ne < Nmax ? ne : 0)) * kL2) * 4;
-    tg[0] = bload2(tgr, ok ? base + 16 * q : kBufOff);
-    tg[1] = bload2(tgr, ok ? base + 16 * q + 8 : kBufOff);
-    tg[2] = bload2(tgr, ok && q < 2 ? base + 64 + 16 * q : kBufOff);
-    tg[3] = bload2(tgr, ok && q < 2 ? base + 64 + 16 * q + 8 : kBufOff);
+    load_targets(tgr, Nmax, fb, fl, t, ok, L, q, tg);
   };
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float lsum = 0.f;
-  f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // GRAD: the frame's dM (pred_tile)
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
     scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});
-    int nitems;
+    const int nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;   // forward
+    // GRAD: this producer's frames pw, pw + NP, ... < gend of the chunk (the
+    // last R frames of the last chunk go to the recurrence waves)
+    const int R = GRAD && fb + lay.fc >= c.nf ? grad_rec_frames(cnt, NP) : 0;
+    const int gend = cnt - R;
+    // the first tiles' targets: in flight during the heads (GRAD: one buffer
+    // and the balancing stores, see grad_frames)
     if (GRAD) {
-      const int nfr = cnt > pw ? (cnt - pw + NP - 1) / NP : 0;
-      nitems = nfr * ntact;
+      load_targets(tgr, Nmax, fb, pw, 0, pw < gend, L, q, tgA);
+      balance_stores(a);
     } else {
-      nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;
-    }
-    // the first tiles' targets: in flight during the heads.  GRAD: one
-    // buffer, then eight dummy stores (out of range) so that every wait on a
-    // target load in the tile loop has the same eight younger stores before
-    // it and the compiler's counts stay exact (vmcnt(8), not vmcnt(0))
-    load_item(fb, nitems, 0, tgA);
-    if (GRAD) {
-      asm volatile("" ::: "memory");
-      const brsrc none = make_brsrc(a.targets, 0u);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) bstore(none, kBufOff, 0.f);
-    } else {
+      load_item(fb, nitems, 0, tgA);
       load_item(fb, nitems, 1, tgB);
     }
     // Rm = Wr @ Rel, Rel = Ve * Ve (train.py:194-195, g2k_lstm_mcr.py:106):
@@ -987,108 +1102,44 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       __builtin_amdgcn_s_setprio(0);
     }
     // phase 2 — predictions and errors (GRAD: and the gradient)
-    float* ys = c.sY + pw * kL2 * kYP;
-    auto item = [&](int k, float2 (&tg)[4], auto after_targets) {
-      int fl, t;
-      item_ft(k, fl, t);
-      const int f = fb + fl;
-      poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)
-      const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : a.targets,
-                                  a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
-      f32x4 dWoT;
-      pred_tile<GRAD>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
-                      c.nact, t, L, q, acc, lsum, dm, dWoT, after_targets);
-      if (GRAD) {
-        // dWo^T[n0 + 4q + v][t = L]: one copy per producer, or one copy
-        // added to in frame order (tile sequence word) when that is too big
-        const int nb = 16 * t + 4 * q;
-        float* dst = c.sGdWo + (lay.dwo_seq ? 0 : pw * Nmax * kT);
-        if (lay.dwo_seq) poll_word(c.sGseq + 2 + t, f);
-        if (L < kT) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            if (nb + v < Nmax) dst[(nb + v) * kT + L] += dWoT[v];
-        }
-        if (lay.dwo_seq) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (lane == 0) lds_store_flag(c.sGseq + 2 + t, f + 1);
-        }
-      }
-    };
     if (GRAD) {
-      // frame by frame, tile by tile, one target buffer: each tile loads the
-      // next tile's targets (this frame's next tile, else the next frame's
-      // first) as soon as its own are consumed, then stores its predictions
-      const int nfr = nitems / (ntact > 0 ? ntact : 1);
-      float2 (&tg)[4] = tgA;
-      for (int fi = 0; fi < nfr; ++fi) {
-        for (int t = 0; t < ntact; ++t) {
-          const int k = fi * ntact + t;
-          item(k, tg, [&] { load_item(fb, nitems, k + 1, tg); });
-        }
-        // the frame's dM to this wave's scratch (M's physical rows), then its terms
-        if (L < kT) {
-          float* dMs = c.sGFrame + pw * kGFrame + kGT_DM;
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            dMs[mrow(4 * q + v) * kT + L] = dm[0][v];
-            if (q < 2) dMs[mrow(16 + 4 * q + v) * kT + L] = dm[1][v];
-          }
-        }
-        frame_grad(a, lay, c, pw + fi * NP, dm);
-        dm[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dm[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      // every producer done with the chunk's frames -> add the ring
+      grad_frames(a, lay, c, pw, fb, pw, NP, gend, act_bits, acc, lsum, tgA, true);
+      // every worker done with the chunk's frames -> its dU rows into dV
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) atomicAdd(c.sGseq, 1);
-      poll_word(c.sGseq, NP * (fb / lay.fc + 1));
+      poll_word(c.sGseq, NP * (fb / lay.fc + 1) + R);    // the recurrence waves add R at the end
       if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)
     } else {
+      f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // (unused by the forward tiles)
+      auto item = [&](int k, float2 (&tg)[4]) {
+        int fl, t;
+        item_ft(k, fl, t);
+        const int f = fb + fl;
+        poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)
+        const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : a.targets,
+                                    a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
+        f32x4 dWoT;
+        pred_tile<false>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tg, (act_bits >> t) & 1u, Nmax,
+                         c.nact, t, L, q, acc, lsum, dm, dWoT, [] {});
+      };
       for (int k = 0; k < nitems; k += 2) {
-        item(k, tgA, [] {});
+        item(k, tgA);
         load_item(fb, nitems, k + 2, tgA);
         if (k + 1 < nitems) {
-          item(k + 1, tgB, [] {});
+          item(k + 1, tgB);
           load_item(fb, nitems, k + 3, tgB);
         }
       }
     }
     if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
   }
-  // metrics (and the loss): each producer publishes its partial sums, then
-  // takes a ticket (LDS atomic); the wave drawing the last ticket sums the
-  // NP rows in producer order (deterministic) and writes the scene's row
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const float v = wave_sum(acc[k]);
-    if (lane == 0) c.sMet[pw * 8 + k] = v;
-  }
-  if (GRAD) {
-    const float v = wave_sum(lsum);
-    if (lane == 0) c.sMet[pw * 8 + 5] = v;
-  }
-  int ticket = 0;
-  if (lane == 0) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // partials before the ticket
-    ticket = atomicAdd(c.sTicket, 1);
-  }
-  ticket = __builtin_amdgcn_readfirstlane(ticket);
-  if (ticket == NP - 1 && lane < 8 && a.metrics) {
-    float v = 0.f;
-    if (lane < 5) {
-      if (c.nf > 0)
-        for (int p = 0; p < NP; ++p) v += c.sMet[p * 8 + lane];
-    } else if (lane == 5) {
-      v = (float)c.nf;
-    }
-    a.metrics[(size_t)s * 8 + lane] = v;
-  }
+  // metrics (and the loss): GRAD also the recurrence waves' rows (NP + w)
+  publish_metrics(a, c, pw, GRAD ? NP + kRecW : NP, acc, lsum, GRAD);
   if (!GRAD) return;
   // GRAD: every producer has added its frames once the ticket count is NP;
   // then the scene's gradient row [P + 2] (g2k_weights order) is formed by
   // all producers together
-  poll_word(c.sTicket, NP);
+  poll_word(c.sTicket, NP + kRecW);
   grad_priv_sum(c, NP);                                // then all producers see sGAcc
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) atomicAdd(c.sGseq + 1, 1);
@@ -1173,16 +1224,39 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       if (lay.dwo_seq) {
         x = c.sGdWo[nn * kT + t];
       } else {
-        for (int pr = 0; pr < NP; ++pr) x += c.sGdWo[(pr * Nmax + nn) * kT + t];
+        for (int pr = 0; pr < NP + kRecW; ++pr) x += c.sGdWo[(pr * Nmax + nn) * kT + t];
       }
-    } else if (p == P) {                              // loss = 1/2 sum dY^2, producer order
-      for (int pr = 0; pr < NP; ++pr) x += c.sMet[pr * 8 + 5];
+    } else if (p == P) {                              // loss = 1/2 sum dY^2, worker order
+      for (int pr = 0; pr < NP + kRecW; ++pr) x += c.sMet[pr * 8 + 5];
       x *= 0.5f;
     } else {                                          // count of (frame, pedestrian) pairs
-      for (int pr = 0; pr < NP; ++pr) x += c.sMet[pr * 8 + 1];
+      for (int pr = 0; pr < NP + kRecW; ++pr) x += c.sMet[pr * 8 + 1];
     }
     row[p] = x;
   }
+}
+
+// GRAD, recurrence wave w after its recurrence: the last R frames of the
+// last chunk (frame cnt - R + w) as gradient worker NP + w, then its metrics
+// row and ticket (with zero partials when R = 0).
+template <int NP>
+__device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayout& lay,
+                                              const SceneCtx& c) {
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float lsum = 0.f;
+  if (c.nf > 0) {
+    const int fb = ((c.nf - 1) / lay.fc) * lay.fc;
+    const int cnt = c.nf - fb;
+    const int R = grad_rec_frames(cnt, NP);
+    if (R > 0) {
+      float2 tg[4];
+      grad_frames(a, lay, c, NP + c.wv, fb, cnt - R + c.wv, R, cnt, scene_act_bits(a, c), acc, lsum,
+                  tg, false);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (c.lane == 0) atomicAdd(c.sGseq, 1);
+    }
+  }
+  publish_metrics(a, c, NP + c.wv, NP + kRecW, acc, lsum, true);
 }
 
 template <int TPW, int NP, bool GRAD>
@@ -1250,9 +1324,10 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.nf = a.n_frames ? clampi(a.n_frames[c.s], 0, F) : F;
   c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians
   if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
-  if (c.wv < kRecW)
+  if (c.wv < kRecW) {
     scene_recurrence<TPW, NP>(a, lay, c);
-  else
+    if (GRAD) rec_grad_work<NP>(a, lay, c);
+  } else
     scene_producer<NP, GRAD>(a, lay, c);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
 }

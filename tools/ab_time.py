@@ -43,8 +43,8 @@ STAMPS = [
      "    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});\n    G2K_ST(1, " + P0 + " && fb == 0);"),
     ("    // phase 2 — predictions and errors (GRAD: and the gradient)",
      "    G2K_ST(2, " + P0 + " && fb == 0);\n    // phase 2 — predictions and errors (GRAD: and the gradient)"),
-    ("        frame_grad(a, lay, c, pw + fi * NP);",
-     "        G2K_ST(3 + fi, " + P0 + " && fb == 0 && fi < 5);\n        frame_grad(a, lay, c, pw + fi * NP);\n        G2K_ST(8 + fi, " + P0 + " && fb == 0 && fi < 4);"),
+    ("        frame_grad(a, lay, c, pw + fi * NP, dm);",
+     "        G2K_ST(3 + fi, " + P0 + " && fb == 0 && fi < 5);\n        frame_grad(a, lay, c, pw + fi * NP, dm);\n        G2K_ST(8 + fi, " + P0 + " && fb == 0 && fi < 4);"),
     ("      poll_word(c.sGseq, NP * (fb / lay.fc + 1));",
      "      G2K_ST(24 + pw, fb == 0);\n      poll_word(c.sGseq, NP * (fb / lay.fc + 1));\n      G2K_ST(12, " + P0 + " && fb == 0);"),
     ("      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)",
@@ -68,9 +68,9 @@ STAMPS = [
     ("        lds_store_flag(c.sFlag + fl, f + 1);\n      }\n", "        lds_store_flag(c.sFlag + fl, f + 1);\n      }\n      G2K_ST(32 + 3 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n"),
 ]
 TILE = [
-    ("f32x4 (&dm)[2], f32x4& dWoT) {", "f32x4 (&dm)[2], f32x4& dWoT, const StepArgs& a, const SceneCtx& c) {\n  G2K_ST(40, " + P0 + " && t == 0);"),
-    ("c.nact, t, L, q, acc, lsum, dm, dWoT);", "c.nact, t, L, q, acc, lsum, dm, dWoT, a, c);"),
-    ("  if (pr && n < nact) {", "  G2K_ST(41, " + P0 + " && t == 0);\n  if (pr && n < nact) {"),
+    ("f32x4 (&dm)[2], f32x4& dWoT, AfterTargets after_targets) {", "f32x4 (&dm)[2], f32x4& dWoT, AfterTargets after_targets, const StepArgs& a, const SceneCtx& c) {\n  G2K_ST(40, " + P0 + " && t == 0);"),
+    ("c.nact, t, L, q, acc, lsum, dm, dWoT, after_targets);", "c.nact, t, L, q, acc, lsum, dm, dWoT, after_targets, a, c);"),
+    ("  after_targets();\n", "  G2K_ST(41, " + P0 + " && t == 0);\n  after_targets();\n"),
     ("  // errors: d = Y - target", "  G2K_ST(42, " + P0 + " && t == 0);\n  // errors: d = Y - target"),
     ("    // dY into the scratch [r][n]", "    G2K_ST(43, " + P0 + " && t == 0);\n    // dY into the scratch [r][n]"),
     ("    wave_lds_sync();\n    // dm += dY", "    G2K_ST(44, " + P0 + " && t == 0);\n    wave_lds_sync();\n    // dm += dY"),
@@ -84,7 +84,7 @@ VARIANTS = {
     "base": {},
     "no_finalize": {SCENE: [("  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);",
                              "  return;\n  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);")]},
-    "no_frame_grad": {SCENE: [("        frame_grad(a, lay, c, pw + fi * NP);", "")]},
+    "no_frame_grad": {SCENE: [("        frame_grad(a, lay, c, pw + fi * NP, dm);", "")]},
     "no_tile_grad": {SCENE: [("  if (GRAD) {\n#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      d0[v] = has_t",
                               "  dWoT = f32x4{0.f, 0.f, 0.f, 0.f};\n  if (false) {\n#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      d0[v] = has_t")]},
     "stamps": {SCENE: STAMPS},
