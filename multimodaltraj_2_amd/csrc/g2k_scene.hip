@@ -901,10 +901,12 @@ __device__ __forceinline__ int grad_rec_frames(int cnt, int NP) { return cnt >= 
 
 // The targets of tile t of chunk frame fl in pred_tile's order (pedestrian
 // 16 t + L, floats 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row, zero
-// for q >= 2) by range-checked buffer loads (no branch: !ok reads zeros).
-__device__ __forceinline__ void load_targets(brsrc tgr, int Nmax, int fb, int fl, int t, bool ok,
-                                             int L, int q, float2 (&tg)[4]) {
+// for q >= 2) by range-checked buffer loads (no branch: !ok and inactive
+// pedestrians n >= n_active read zeros without touching memory).
+__device__ __forceinline__ void load_targets(brsrc tgr, int Nmax, int nact, int fb, int fl, int t,
+                                             bool ok, int L, int q, float2 (&tg)[4]) {
   const int ne = 16 * t + L;
+  ok = ok && ne < nact;
   const int base = (((fb + fl) * Nmax + (ne < Nmax ? ne : 0)) * kL2) * 4;
   tg[0] = bload2(tgr, ok ? base + 16 * q : kBufOff);
   tg[1] = bload2(tgr, ok ? base + 16 * q + 8 : kBufOff);
@@ -942,7 +944,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
   const int Nmax = a.d.Nmax, F = a.d.F, L = c.L, q = c.q, ntact = c.ntact;
   const brsrc tgr = scene_targets_rsrc(a, c.s);
   if (!preloaded) {
-    load_targets(tgr, Nmax, fb, f0, 0, f0 < fend, L, q, tg);
+    load_targets(tgr, Nmax, c.nact, fb, f0, 0, f0 < fend, L, q, tg);
     balance_stores(a);
   }
   float* ys = c.sY + slot * kL2 * kYP;
@@ -958,7 +960,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
       f32x4 dWoT;
       pred_tile<true>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
                       c.nact, t, L, q, acc, lsum, dm, dWoT,
-                      [&] { load_targets(tgr, Nmax, fb, nfl, nt, nfl < fend, L, q, tg); });
+                      [&] { load_targets(tgr, Nmax, c.nact, fb, nfl, nt, nfl < fend, L, q, tg); });
       // dWo^T[n0 + 4q + v][t = L]: one copy per worker, or one copy added
       // to in frame order (tile sequence word) when that is too big
       const int nb = 16 * t + 4 * q;
@@ -1045,7 +1047,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     const bool ok = k < nitems;
     int fl, t;
     item_ft(ok ? k : 0, fl, t);
-    load_targets(tgr, Nmax, fb, fl, t, ok, L, q, tg);
+    load_targets(tgr, Nmax, c.nact, fb, fl, t, ok, L, q, tg);
   };
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float lsum = 0.f;
@@ -1061,7 +1063,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // the first tiles' targets: in flight during the heads (GRAD: one buffer
     // and the balancing stores, see grad_frames)
     if (GRAD) {
-      load_targets(tgr, Nmax, fb, pw, 0, pw < gend, L, q, tgA);
+      load_targets(tgr, Nmax, c.nact, fb, pw, 0, pw < gend, L, q, tgA);
       balance_stores(a);
     } else {
       load_item(fb, nitems, 0, tgA);
