@@ -332,6 +332,17 @@ __device__ __forceinline__ void poll_flag(const int* flag, int want) {
 
 __host__ __device__ inline int rup4(int x) { return (x + 3) & ~3; }
 
+// Per-lane select written as bit operations (it compiles to v_cndmask_b32).
+// Left to itself the compiler turns a chain of ternaries on the lane index
+// (a switch) or a ternary between loaded values into exec-masked branches:
+// several scalar instructions per case, and an LDS round trip per masked
+// load.  (Not inline asm: the hazard recognizer does not see an asm VALU
+// write that an MFMA then reads.)
+__device__ __forceinline__ float lane_sel(bool c, float a, float b) {
+  const int m = -(int)c;
+  return __int_as_float((__float_as_int(a) & m) | (__float_as_int(b) & ~m));
+}
+
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {

@@ -78,10 +78,136 @@ TILE = [
     ("      poll_flag(c.sMflag + fl, f + 1);         // M of this frame", "      G2K_ST(46, " + P0 + " && t == 0);\n      poll_flag(c.sMflag + fl, f + 1);         // M of this frame"),
     ("        if (lay.dwo_seq) {\n          asm volatile", "        G2K_ST(47, " + P0 + " && t == 0);\n        if (lay.dwo_seq) {\n          asm volatile"),
 ]
+# forward timeline: scene's producer 0 (P0) and recurrence wave 0 (R0);
+# slot 27 / 28: s_memrealtime (100 MHz) at start / end of R0 (dispatch skew)
+R0 = "c.wv == 0"
+TL_FWD = [
+    ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
+    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+     "  G2K_ST(0, c.tid == 0);\n  if (c.wv == 0 && c.lane == 0) g2k_stamp_buf[(size_t)c.s * 64 + 27] = (unsigned)__builtin_amdgcn_s_memrealtime();\n"
+     "  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
+     "    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first\n    G2K_ST(1, " + P0 + ");"),
+    ("  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians",
+     "  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians\n  G2K_ST(3, " + P0 + ");"),
+    ("  __syncthreads();                                              // B1: window + weights landed",
+     "  G2K_ST(4, " + P0 + " && fb == 0);\n  __syncthreads();\n  G2K_ST(5, " + P0 + " && fb == 0);"),
+    ("  __syncthreads();                                              // B2: V, VG, K1, K2",
+     "  G2K_ST(51, " + P0 + " && fb == 0);\n  __syncthreads();\n  G2K_ST(6, " + P0 + " && fb == 0);"),
+    ("      const FrameHeadOut hd =", "      G2K_ST(7 + 2 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n      const FrameHeadOut hd ="),
+    ("      if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n", "      if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      G2K_ST(8 + 2 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n"),
+    ("        poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)",
+     "        G2K_ST(13 + 2 * k, " + P0 + " && k < 6);\n        poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)\n        G2K_ST(14 + 2 * k, " + P0 + " && k < 6);"),
+    ("  publish_metrics(a, c, pw, GRAD ? NP + kRecW : NP, acc, lsum, GRAD);",
+     "  G2K_ST(25, " + P0 + ");\n  publish_metrics(a, c, pw, GRAD ? NP + kRecW : NP, acc, lsum, GRAD);\n  G2K_ST(50, " + P0 + ");"),
+    ("        rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,\n                    as_lane + fn * kD * kD, fln, bn);",
+     "        rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,\n                    as_lane + fn * kD * kD, fln, bn);\n        G2K_ST(30 + g, " + R0 + " && g < 20);"),
+    ("  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L,\n           c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);",
+     "  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L,\n           c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);\n  G2K_ST(26, " + R0 + ");\n"
+     "  if (c.wv == 0 && c.lane == 0) g2k_stamp_buf[(size_t)c.s * 64 + 28] = (unsigned)__builtin_amdgcn_s_memrealtime();"),
+    ("    scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, live, [&] {",
+     "    G2K_ST(52, " + R0 + " && fb == 0);\n    scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, live, [&] {"),
+]
+
+
+# one frame of the recurrence in detail (g = 17, 18): R0 before / after its
+# poll, every wave's publish
+TL_REC = TL_FWD + [
+    ("        poll_red(seq + (c.L & 3), g + 2, c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, z);",
+     "        G2K_ST(53, " + R0 + " && g == 17);\n"
+     "        poll_red(seq + (c.L & 3), g + 2, c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, z);\n"
+     "        G2K_ST(54, " + R0 + " && g == 17);\n        G2K_ST(59, " + R0 + " && g == 18);"),
+    ("        G2K_ST(30 + g, " + R0 + " && g < 20);",
+     "        G2K_ST(30 + g, " + R0 + " && g < 20);\n        G2K_ST(55 + c.wv, c.wv > 0 && g == 17);"),
+]
+
+
+# the same stamps kept in LDS (no global store, so no vmcnt wait behind a
+# stamp) and copied out after a final barrier
+LDS_STAMP_DEF = """
+__device__ unsigned g2k_stamp_buf[4096 * 64];
+__shared__ unsigned g2k_lds_stamp[64];
+#define G2K_ST(k, cond) do { if ((cond) && (threadIdx.x & 63) == 0) { \\
+  g2k_lds_stamp[(k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
+"""
+HEAD_ST = "__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 4 && wrow0 == 0"
+
+
+def lds_stamps(reps):
+    out = []
+    for a, b in reps:
+        b = b.replace(STAMP_DEF, LDS_STAMP_DEF)
+        b = b.replace("g2k_stamp_buf[(size_t)c.s * 64 + 27]", "g2k_lds_stamp[27]")
+        b = b.replace("g2k_stamp_buf[(size_t)c.s * 64 + 28]", "g2k_lds_stamp[28]")
+        out.append((a, b))
+    out += [
+        ('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup',
+         '  __syncthreads();\n  if (c.tid < 64) g2k_stamp_buf[(size_t)c.s * 64 + c.tid] = g2k_lds_stamp[c.tid];\n'
+         '  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup'),
+        ("  f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);",
+         "  G2K_ST(60, " + HEAD_ST + ");\n  f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);"),
+        ("  __builtin_amdgcn_sched_barrier(0);\n  attn_weights(aA, as_dst, L, q);",
+         "  G2K_ST(61, " + HEAD_ST + " && aA[0] != 12345.f);\n  __builtin_amdgcn_sched_barrier(0);\n  attn_weights(aA, as_dst, L, q);"),
+        ("  if ((threadIdx.x & 63) == 0) lds_store_flag(as_flag, flag_val);",
+         "  if ((threadIdx.x & 63) == 0) lds_store_flag(as_flag, flag_val);\n  G2K_ST(62, " + HEAD_ST + ");"),
+    ]
+    return out
+
+
+# I-cache experiment: every producer runs the staging and frame-head code once
+# on whatever LDS holds while the prologue's DMA is in flight
+WARM = [
+    ("  if (VMC > 0 && fb == 0 && hl) asm volatile(\"s_waitcnt vmcnt(%0)\" ::\"n\"(VMC) : \"memory\");",
+     "  if (fb == 0 && c.wv >= kRecW) {\n"
+     "    scene_vtile(a, lay, c, 0, wcc);\n    scene_kmats(c);\n    float rm0[4] = {0.f, 0.f, 0.f, 0.f};\n"
+     "    (void)frame_head(c.sm, c.sV, c.sVG, 0, lay.wcmax, rm0, a.lambda, c.sRing + (c.wv - kRecW) * kD * kD, reinterpret_cast<int*>(c.sm + SM_SPARE), 0,\n"
+     "                     nullptr, nullptr, nullptr, c.L, c.q);\n  }\n"
+     "  if (VMC > 0 && fb == 0 && hl) asm volatile(\"s_waitcnt vmcnt(%0)\" ::\"n\"(VMC) : \"memory\");"),
+]
+
+
+def tl_rec_print(st, t):
+    import numpy as np
+    tl_fwd_print(st, t)
+    rel = (st - st[:, :1]) % (1 << 32)
+    med = np.median(rel, axis=0)
+    print("frame 17 (median): R0 poll start", int(med[53]), "poll end", int(med[54]), "R0 published",
+          int(med[47]), "waves 1-3 published", [int(med[56 + w]) for w in range(3)],
+          "R0 frame 18 poll end", int(med[59]))
+
+
+def tl_fwd_print(st, t):
+    import numpy as np
+    S = st.shape[0]
+    rs = st[:, 27]
+    re = st[:, 28]
+    t0 = rs.min()
+    print("realtime (10 ns ticks) start spread: min 0 max", int(rs.max() - t0),
+          " end: min", int(re.min() - t0), "max", int(re.max() - t0),
+          " median duration", float(np.median(re - rs)))
+    names = {1: "dma issued", 3: "nact", 4: "B1 wait", 5: "B1", 51: "stage done", 6: "B2",
+             7: "h0s", 8: "h0e", 9: "h1s", 10: "h1e", 11: "h2s", 12: "h2e", 25: "prod done",
+             50: "published", 52: "R0 at stage", 26: "recur stored"}
+    for sc in (0, S // 2, S - 1):
+        r = st[sc]
+        rel = (r - r[0]) % (1 << 32)
+        print(f"scene {sc} n_active {int(t['n_active'][sc])}: " +
+              "  ".join(f"{v}:{rel[k]}" for k, v in names.items()))
+        print("   items (poll start, poll end):", " ".join(f"({rel[13 + 2 * k]},{rel[14 + 2 * k]})" for k in range(6)))
+        print("   recurrence frame ends:", " ".join(str(rel[30 + g]) for g in range(20)))
+    # medians over scenes
+    rel = (st - st[:, :1]) % (1 << 32)
+    med = np.median(rel, axis=0)
+    print("median:", "  ".join(f"{v}:{int(med[k])}" for k, v in names.items()))
+    print("median recurrence frame ends:", " ".join(str(int(med[30 + g])) for g in range(20)))
+    print("median items:", " ".join(f"({int(med[13 + 2 * k])},{int(med[14 + 2 * k])})" for k in range(6)))
+
+
 NO_RECUR = [("  const bool live = a.h_in != nullptr;", "  const bool live = false;")]
 NO_RECUR_SCENE = {SCENE: NO_RECUR}
 VARIANTS = {
     "base": {},
+    "orig": {},
     "no_finalize": {SCENE: [("  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);",
                              "  return;\n  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);")]},
     "no_frame_grad": {SCENE: [("        frame_grad(a, lay, c, pw + fi * NP, dm);", "")]},
@@ -95,6 +221,11 @@ VARIANTS = {
     "stamps_nolsr": {SCENE: STAMPS, "__flags__": ["-mllvm", "-disable-lsr"]},
     "stamps_tile": {SCENE: STAMPS + TILE},
     "stamps_fwd": {SCENE: STAMPS},
+    "tl_fwd": {SCENE: TL_FWD},
+    "tl_rec": {SCENE: TL_REC},
+    "tl_lds": {SCENE: lds_stamps(TL_REC)},
+    "warm": {SCENE: WARM},
+    "tl_lds_warm": {SCENE: lds_stamps(TL_REC) + WARM},
 }
 
 
@@ -103,6 +234,11 @@ def build_variant(name):
     tmp = tempfile.mkdtemp(prefix=f"g2k_{name}_")
     for f in os.listdir(src):
         shutil.copy(os.path.join(src, f), tmp)
+        if name == "orig" and f.endswith((".hip", ".h")):   # the committed sources
+            git = subprocess.run(["git", "-C", ROOT, "show", "HEAD:multimodaltraj_2_amd/csrc/" + f],
+                                 capture_output=True, text=True)
+            if git.returncode == 0:
+                open(os.path.join(tmp, f), "w").write(git.stdout)
     for fname, reps in VARIANTS[name].items():
         if fname == "__flags__":
             continue
@@ -111,7 +247,7 @@ def build_variant(name):
         for a, b in reps:
             assert a in s, (name, a[:60])
             s = s.replace(a, b)
-        if name.startswith("stamps") and fname == SCENE:
+        if (name.startswith("stamps") or name.startswith("tl_")) and fname == SCENE:
             s += STAMP_EXPORT
         open(p, "w").write(s)
     out = f"/tmp/libg2k_{name}.so"
@@ -186,6 +322,25 @@ def main():
     for name in names:
         lib = _lib.load(build_variant(name))
         _lib._lib = lib
+        if name.startswith("tl_"):
+            import numpy as np
+            lib.g2k_stamp_copy.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            params = fs.init_params(c["Nmax"], seed=0, device=dev)
+            plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+            for _ in range(5):
+                plan.run()
+            torch.cuda.synchronize()
+            buf = (ctypes.c_uint * (S * 64))()
+            assert lib.g2k_stamp_copy(buf, S * 64) == 0
+            st = np.frombuffer(buf, dtype=np.uint32).reshape(S, 64).astype(np.int64)
+            (tl_rec_print if name.startswith("tl_rec") or name.startswith("tl_lds") else tl_fwd_print)(st, t)
+            print(f"{name}: fwd {time_it(plan.run):7.2f} us (stamped build)")
+            if name.startswith("tl_lds"):
+                rel = (st - st[:, :1]) % (1 << 32)
+                med = np.median(rel, axis=0)
+                print("head 0 (median): operands", int(med[60]), "A done", int(med[61]), "attn done",
+                      int(med[62]))
+            continue
         if name.startswith("stamps"):
             lib.g2k_stamp_copy.argtypes = [ctypes.c_void_p, ctypes.c_int]
             stamps(lib, c, t, dev, train=not name.endswith("_fwd"))
