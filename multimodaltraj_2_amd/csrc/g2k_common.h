@@ -48,6 +48,17 @@ __device__ __forceinline__ brsrc make_brsrc(const void* base, uint32_t bytes) {
 __device__ __forceinline__ void bstore(brsrc r, int off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
+__device__ __forceinline__ void bstore4(brsrc r, int off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(
+      (__attribute__((ext_vector_type(4))) unsigned){__float_as_uint(v.x), __float_as_uint(v.y),
+                                                      __float_as_uint(v.z), __float_as_uint(v.w)},
+      r, off, 0, 0);
+}
+__device__ __forceinline__ float4 bload4(brsrc r, int off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                     __uint_as_float(v[3]));
+}
 __device__ __forceinline__ float2 bload2(brsrc r, int off) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
   return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
@@ -331,6 +342,14 @@ __device__ __forceinline__ void poll_flag(const int* flag, int want) {
 }
 
 __host__ __device__ inline int rup4(int x) { return (x + 3) & ~3; }
+
+// One int at a wave-uniform address by a scalar load (scalar cache), not
+// through the CU's vector-memory pipeline; for data the kernel never writes.
+__device__ __forceinline__ int sload_i32(const int32_t* p) {
+  int v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
 
 // Per-lane select written as bit operations (it compiles to v_cndmask_b32).
 // Left to itself the compiler turns a chain of ternaries on the lane index

@@ -47,6 +47,11 @@ constexpr int SM_SPARE = 1084;  // write-only word (stores of lanes without an e
 constexpr int kSceneSmall = 1088;
 constexpr int kKA = 12;       // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
 constexpr int kYP = 17;       // train: per-producer dY tile scratch [24][kYP] (pitch: bank spread)
+// per-worker tile scratch (floats): the prediction tile transposed for its
+// 16-byte stores ([28][16]: 24 pred rows + 4 rows that lanes without a row
+// write), then (train) the dY tile [24][kYP]
+constexpr int kYS = 448;
+constexpr int kTileStores = 8;   // global stores per prediction tile (4-byte path)
 // train mode
 constexpr int kGFrame = 192;  // per-producer frame scratch: dM [24][8] (frame_grad's P6)
 constexpr int kGT_DM = 0;
@@ -69,7 +74,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   SceneLayout s;
   s.fc = fc;
   s.wcmax = (fc - 1) * stride + kT;
-  s.pp = 2 * Nmax + 4;                        // padded rows: lanes reading across rows spread banks
+  s.pp = 2 * Nmax;                            // unpadded: the chunk's rows are one contiguous copy
   int o = 0;
   s.o_wi = o;    o += rup4(Nmax * kD);
   s.o_wo = o;    o += rup4(kT * Nmax);
@@ -77,7 +82,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
   const int NG = NP + kRecW;                          // train: producers + recurrence waves
-  s.o_y = o;     o += grad ? NG * kL2 * kYP : 0;      // dY tile scratch (train)
+  s.o_y = o;     o += (grad ? NG : (NP == 8 ? NP : 0)) * kYS;   // tile scratch (store transpose, dY)
   s.o_met = o;   o += (grad ? NG : NP) * 8;
   s.o_ring = o;  o += fc * kD * kD;
   s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
@@ -306,7 +311,8 @@ struct SceneCtx {
 };
 
 // LDS-DMA of a chunk's position window rows (train.py:76-79 window) into
-// rows of pitch lay.pp: wave w issues rows w, w + waves, ...
+// rows of pitch lay.pp = 2 Nmax: one contiguous 16-byte-per-lane copy, or (odd
+// Nmax / unaligned input) wave w issues rows w, w + waves, ... by 4 bytes
 template <int NT>
 __device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneLayout& lay,
                                               const SceneCtx& c, int fb, int cnt) {
@@ -314,18 +320,20 @@ __device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneLayo
   const int wcc = (cnt - 1) * stride + kT;
   const float* src = a.pos + ((size_t)c.s * a.d.W + fb * stride) * Nmax * 2;
   const bool wide = (Nmax & 1) == 0 && (((uintptr_t)a.pos) & 15) == 0;
+  if (wide) {
+    // the chunk's rows are contiguous in both places: 1-KiB instructions
+    // (per-row 256-B ones were 4x the instructions through the CU's
+    // vector-memory pipeline, which the whole prologue queues on)
+    dma_copy_n<NT>(src, c.sPos, wcc * Nmax / 2, c.wv, c.lane);
+    return;
+  }
   for (int r = c.wv; r < wcc; r += NT / 64) {
     const float* g = src + (size_t)r * Nmax * 2;
     float* d = c.sPos + r * lay.pp;
-    if (wide) {
-      for (int i = 0; i < Nmax / 2; i += 64)
-        if (i + c.lane < Nmax / 2) dma16(g + 4 * (i + c.lane), d + 4 * i);
-    } else {
-      for (int i = 0; i < 2 * Nmax; i += 64)
-        if (i + c.lane < 2 * Nmax)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + i + c.lane),
-                                           (__attribute__((address_space(3))) void*)(d + i), 4, 0, 0);
-    }
+    for (int i = 0; i < 2 * Nmax; i += 64)
+      if (i + c.lane < 2 * Nmax)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + i + c.lane),
+                                         (__attribute__((address_space(3))) void*)(d + i), 4, 0, 0);
   }
 }
 
@@ -573,7 +581,7 @@ __device__ __forceinline__ int mrow(int r) { return (r & 1) * kL + (r >> 1); }
 // `after_targets` runs once the target registers are consumed (GRAD: the
 // next tile's targets are loaded into them there, before this tile's stores,
 // so the next tile's wait counts exactly those stores).
-template <bool GRAD, typename AfterTargets>
+template <bool GRAD, bool TS, typename AfterTargets>
 __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, brsrc pr,
                                           const float2 (&tg)[4], bool has_t, int Nmax, int nact,
                                           int t, int L, int q, float acc[5], float& lsum,
@@ -593,15 +601,6 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
       a1[ks] = M[mrow(16 + L7) * kT + k];                  // A[r = 16 + L][k]
       wo[ks] = sWo[k * Nmax + nc];                         // B[k][n = n0 + L]
     }
-    if (GRAD) {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        bm[ks] = M[mrow(4 * q + ks) * kT + L7];
-        bm[4 + ks] = M[mrow(16 + 4 * (q & 1) + ks) * kT + L7];
-      }
-      asm volatile("" : "+v"(bm[0]), "+v"(bm[1]), "+v"(bm[2]), "+v"(bm[3]), "+v"(bm[4]), "+v"(bm[5]),
-                   "+v"(bm[6]), "+v"(bm[7]));
-    }
     asm volatile("" : "+v"(a0[0]), "+v"(a0[1]), "+v"(a1[0]), "+v"(a1[1]), "+v"(wo[0]), "+v"(wo[1]));
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -620,14 +619,44 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
   }
   after_targets();
   asm volatile("" ::: "memory");                           // ... then the stores
-  {
-    // range-checked stores (no branch): inactive columns and the block-1
-    // rows of lane groups 2, 3 fall outside the frame's buffer
+  if (TS && (Nmax & 3) == 0) {
+    // the tile transposed through the wave's scratch (physical pred rows x
+    // 16 columns) so that a lane stores four consecutive pedestrians of one
+    // row: two 16-byte stores per lane instead of eight 4-byte ones (the
+    // CU's vector-memory issue is what the producers queue on).  Columns
+    // from n_active up to the next multiple of 4 get Y = 0 (w = 0 there).
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      ys[mrow(4 * q + v) * 16 + L] = y0[v];
+      ys[(hi ? mrow(16 + 4 * q + v) : kL2 + v) * 16 + L] = y1[v];   // rows 24..27: unused
+    }
+    wave_lds_sync();
+    const int lane = L + 16 * q, row = lane >> 2, c4 = 4 * (lane & 3);
+    const float4 s0 = *reinterpret_cast<const float4*>(ys + row * 16 + c4);              // rows 0..15
+    const float4 s1 = *reinterpret_cast<const float4*>(ys + (16 + (row & 7)) * 16 + c4);  // 16..23
+    const bool okc = n0 + c4 < nact;
+    bstore4(pr, okc ? (row * Nmax + n0 + c4) * 4 : kBufOff, s0);
+    bstore4(pr, (okc && lane < 32) ? ((16 + row) * Nmax + n0 + c4) * 4 : kBufOff, s1);
+  } else {
+    // range-checked 4-byte stores (no branch): inactive columns and the
+    // block-1 rows of lane groups 2, 3 fall outside the frame's buffer
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       bstore(pr, n < nact ? (mrow(4 * q + v) * Nmax + n) * 4 : kBufOff, y0[v]);
       bstore(pr, (n < nact && hi) ? (mrow(16 + 4 * q + v) * Nmax + n) * 4 : kBufOff, y1[v]);
     }
+  }
+  if (GRAD) {
+    // M's operand of dWo^T, loaded here (not with Y's operands) so that it is
+    // not live across the stores; its latency hides under the error terms
+    const int L7 = L & 7;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bm[ks] = M[mrow(4 * q + ks) * kT + L7];
+      bm[4 + ks] = M[mrow(16 + 4 * (q & 1) + ks) * kT + L7];
+    }
+    asm volatile("" : "+v"(bm[0]), "+v"(bm[1]), "+v"(bm[2]), "+v"(bm[3]), "+v"(bm[4]), "+v"(bm[5]),
+                 "+v"(bm[6]), "+v"(bm[7]));
   }
   float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f;
 #pragma unroll
@@ -642,19 +671,38 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
       el2 += __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
     }
   }
-  ea += partner16(ea); eb += partner16(eb); ec += partner16(ec); el2 += partner16(el2);
-  ea += partner32(ea); eb += partner32(eb); ec += partner32(ec); el2 += partner32(el2);
-  if (has_t && q == 1) {                   // group 1 holds the last step (r = 22, 23)
+  // el2 needs no sum across lanes: each lane adds its steps' share (the
+  // lanes are summed when the metrics are published)
+  acc[3] = fmaf(has_t ? 1.0f / 12.0f : 0.f, el2, acc[3]);
+  // ea, eb, ec summed over the four lane groups and gathered in group 1 (it
+  // holds step 11, the fde) by five permlane swaps, branch-free after.
+  // permlane32_swap(x, y) -> {[x.lo, y.lo], [x.hi, y.hi]} (32-lane halves);
+  // permlane16_swap(x, y) -> {[x.r0, y.r0, x.r2, y.r2], [x.r1, y.r1, x.r3, y.r3]}
+  auto sw32 = [](float x, float y) {
+    return __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  };
+  auto sw16 = [](float x, float y) {
+    return __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  };
+  const auto p1 = sw32(ea, eb), p2 = sw32(ec, ec);
+  const float s1 = __uint_as_float(p1[0]) + __uint_as_float(p1[1]);   // rows: ea, ea, eb, eb (halves)
+  const float s2 = __uint_as_float(p2[0]) + __uint_as_float(p2[1]);   // ec halves
+  const auto p3 = sw16(s1, s2);
+  const float tt = __uint_as_float(p3[0]) + __uint_as_float(p3[1]);   // rows: ea, ec, eb, ec
+  const auto p4 = sw16(tt, tt);                                       // [0]: rows ea, ea, eb, eb
+  const auto p5 = sw32(__uint_as_float(p4[0]), __uint_as_float(p4[0]));   // [1]: eb everywhere
+  const float sa = __uint_as_float(p4[0]), sb = __uint_as_float(p5[1]), sc = tt;   // row 1
+  {
+    const float g1 = (has_t && q == 1) ? 1.f : 0.f;   // group 1's lanes of pedestrians with targets
     const float fx = d1[2], fy = d1[3];
-    const float hm = 0.5f * (ea - ec);
-    const float lam = 0.5f * (ea + ec) + __builtin_amdgcn_sqrtf(fmaf(hm, hm, eb * eb));
+    const float hm = 0.5f * (sa - sc);
+    const float lam = 0.5f * (sa + sc) + __builtin_amdgcn_sqrtf(fmaf(hm, hm, sb * sb));
     const float fsq = fmaf(fx, fx, fy * fy);
-    acc[0] += __builtin_amdgcn_sqrtf(fmaxf(lam, 0.f)) * (1.0f / 12.0f);
-    acc[1] += 1.0f;
-    acc[2] += fsq;
-    acc[3] += el2 * (1.0f / 12.0f);
-    acc[4] += __builtin_amdgcn_sqrtf(fsq);
-    if (GRAD) lsum += ea + ec;
+    acc[0] = fmaf(g1 * (1.0f / 12.0f), __builtin_amdgcn_sqrtf(fmaxf(lam, 0.f)), acc[0]);
+    acc[1] += g1;
+    acc[2] = fmaf(g1, fsq, acc[2]);
+    acc[4] = fmaf(g1, __builtin_amdgcn_sqrtf(fsq), acc[4]);
+    if (GRAD) lsum = fmaf(g1, sa + sc, lsum);
   }
   if (GRAD) {
 #pragma unroll
@@ -916,10 +964,13 @@ __device__ __forceinline__ void load_targets(brsrc tgr, int Nmax, int nact, int 
   const int ne = 16 * t + L;
   ok = ok && ne < nact;
   const int base = (((fb + fl) * Nmax + (ne < Nmax ? ne : 0)) * kL2) * 4;
-  tg[0] = bload2(tgr, ok ? base + 16 * q : kBufOff);
-  tg[1] = bload2(tgr, ok ? base + 16 * q + 8 : kBufOff);
-  tg[2] = bload2(tgr, ok && q < 2 ? base + 64 + 16 * q : kBufOff);
-  tg[3] = bload2(tgr, ok && q < 2 ? base + 64 + 16 * q + 8 : kBufOff);
+  // two 16-B loads (rows are 96 B: every float4 is 16-B aligned)
+  const float4 u = bload4(tgr, ok ? base + 16 * q : kBufOff);
+  const float4 w = bload4(tgr, ok && q < 2 ? base + 64 + 16 * q : kBufOff);
+  tg[0] = make_float2(u.x, u.y);
+  tg[1] = make_float2(u.z, u.w);
+  tg[2] = make_float2(w.x, w.y);
+  tg[3] = make_float2(w.z, w.w);
 }
 
 __device__ __forceinline__ brsrc scene_targets_rsrc(const StepArgs& a, int s) {
@@ -927,14 +978,15 @@ __device__ __forceinline__ brsrc scene_targets_rsrc(const StepArgs& a, int s) {
                     (uint32_t)a.d.F * a.d.Nmax * kL2 * 4);
 }
 
-// Eight out-of-range stores right after the first target load of a tile loop:
-// every wait on a target load in the loop then has the same eight younger
-// stores before it and the compiler's counts stay exact (vmcnt(8), not 0).
+// kTileStores out-of-range stores right after the first target load of a
+// tile loop: every wait on a target load in the loop then has the same number
+// of younger stores before it (a tile's own) and the compiler's counts stay
+// exact (vmcnt(kTileStores), not 0).
 __device__ __forceinline__ void balance_stores(const StepArgs& a) {
   asm volatile("" ::: "memory");
   const brsrc none = make_brsrc(a.targets, 0u);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) bstore(none, kBufOff, 0.f);
+  for (int i = 0; i < kTileStores; ++i) bstore(none, kBufOff, 0.f);
 }
 
 // GRAD: one gradient worker's frames fl = f0, f0 + fstep, ... < fend of the
@@ -955,7 +1007,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
     load_targets(tgr, Nmax, c.nact, fb, f0, 0, f0 < fend, L, q, tg);
     balance_stores(a);
   }
-  float* ys = c.sY + slot * kL2 * kYP;
+  float* ys = c.sY + slot * kYS;
   f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   for (int fl = f0; fl < fend; fl += fstep) {
     const int f = fb + fl;
@@ -966,7 +1018,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
       const bool nxt = t + 1 < ntact;                    // the next tile: this frame's, else the next frame's
       const int nfl = nxt ? fl : fl + fstep, nt = nxt ? t + 1 : 0;
       f32x4 dWoT;
-      pred_tile<true>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
+      pred_tile<true, false>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
                       c.nact, t, L, q, acc, lsum, dm, dWoT,
                       [&] { load_targets(tgr, Nmax, c.nact, fb, nfl, nt, nfl < fend, L, q, tg); });
       // dWo^T[n0 + 4q + v][t = L]: one copy per worker, or one copy added
@@ -1044,9 +1096,12 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   // tile items of a chunk (forward): item j -> frame j / ntact, tile
   // j % ntact; this producer takes items pw, pw + NP, ...  (GRAD: whole
   // frames per worker, grad_frames)
+  // item j -> (j / ntact, j % ntact) by a reciprocal, no division per item
+  // (exact while j * ntact < 2^16; here j < 32 ntact and ntact <= 16)
+  const uint32_t inv = 65536u / (uint32_t)(ntact > 0 ? ntact : 1) + 1u;
   auto item_ft = [&](int k, int& fl, int& t) {
     const int j = pw + k * NP;
-    fl = j / ntact;
+    fl = (int)(((uint32_t)j * inv) >> 16);
     t = j - fl * ntact;
   };
   const brsrc tgr = scene_targets_rsrc(a, s);
@@ -1128,7 +1183,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
         const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : a.targets,
                                     a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
         f32x4 dWoT;
-        pred_tile<false>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tg, (act_bits >> t) & 1u, Nmax,
+        pred_tile<false, NP == 8>(c.sMring + fl * kL2 * kT, c.sWo, c.sY + pw * kYS, pr, tg, (act_bits >> t) & 1u, Nmax,
                          c.nact, t, L, q, acc, lsum, dm, dWoT, [] {});
       };
       for (int k = 0; k < nitems; k += 2) {
@@ -1325,18 +1380,26 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
         case 8: src = a.vislet + (size_t)c.s * 2 * Nmax; dst = c.sVis; n = Nmax; break;
         default: src = a.vislet + (size_t)c.s * 2 * Nmax + Nmax; dst = c.sVis + Nmax; n = Nmax; break;
       }
-      for (int i = 0; i < n; i += 64)
-        if (i + lane < n)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i + lane),
-                                           (__attribute__((address_space(3))) void*)(dst + i), 4, 0, 0);
+      // 16 bytes per lane when both ends allow it (every segment of the
+      // usual layouts): 11 wave-instructions instead of 26 through the CU's
+      // vector-memory pipeline, which the whole prologue queues on
+      if (((((uintptr_t)src) | lds_addr(dst)) & 15) == 0 && (n & 3) == 0) {
+        for (int i = 0; i < n / 4; i += 64)
+          if (i + lane < n / 4) dma16(src + 4 * (i + lane), dst + 4 * i);
+      } else {
+        for (int i = 0; i < n; i += 64)
+          if (i + lane < n)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i + lane),
+                                             (__attribute__((address_space(3))) void*)(dst + i), 4, 0, 0);
+      }
     }
     if (c.tid < lay.fc) {                                // flags hold (global frame + 1)
       c.sFlag[c.tid] = 0;
       c.sMflag[c.tid] = 0;
     }
   }
-  c.nact = clampi(a.n_active[c.s], 0, Nmax);
-  c.nf = a.n_frames ? clampi(a.n_frames[c.s], 0, F) : F;
+  c.nact = clampi(sload_i32(a.n_active + c.s), 0, Nmax);
+  c.nf = a.n_frames ? clampi(sload_i32(a.n_frames + c.s), 0, F) : F;
   c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians
   if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
   if (c.wv < kRecW) {

@@ -125,8 +125,8 @@ TL_REC = TL_FWD + [
 # the same stamps kept in LDS (no global store, so no vmcnt wait behind a
 # stamp) and copied out after a final barrier
 LDS_STAMP_DEF = """
-__device__ unsigned g2k_stamp_buf[4096 * 64];
-__shared__ unsigned g2k_lds_stamp[64];
+__device__ unsigned g2k_stamp_buf[4096 * 128];
+__shared__ unsigned g2k_lds_stamp[128];
 #define G2K_ST(k, cond) do { if ((cond) && (threadIdx.x & 63) == 0) { \\
   g2k_lds_stamp[(k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
 """
@@ -142,7 +142,7 @@ def lds_stamps(reps):
         out.append((a, b))
     out += [
         ('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup',
-         '  __syncthreads();\n  if (c.tid < 64) g2k_stamp_buf[(size_t)c.s * 64 + c.tid] = g2k_lds_stamp[c.tid];\n'
+         '  __syncthreads();\n  if (c.tid < 128) g2k_stamp_buf[(size_t)c.s * 128 + c.tid] = g2k_lds_stamp[c.tid];\n'
          '  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup'),
         ("  f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);",
          "  G2K_ST(60, " + HEAD_ST + ");\n  f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);"),
@@ -164,6 +164,68 @@ WARM = [
      "                     nullptr, nullptr, nullptr, c.L, c.q);\n  }\n"
      "  if (VMC > 0 && fb == 0 && hl) asm volatile(\"s_waitcnt vmcnt(%0)\" ::\"n\"(VMC) : \"memory\");"),
 ]
+
+
+# inside the forward tile (P0's LAST tile survives): entry, Y done, targets
+# consumed, stores issued, error terms done
+PT = "!GRAD && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 4"
+TL_TILE = [
+    ("  const int n0 = 16 * t, n = n0 + L;\n  const bool hi = q < 2;",
+     "  G2K_ST(40, " + PT + ");\n  const int n0 = 16 * t, n = n0 + L;\n  const bool hi = q < 2;"),
+    ("  // errors: d = Y - target, (x, y) pairs in registers (v = 0, 1 and 2, 3)",
+     "  G2K_ST(41, " + PT + " && y0[0] != 12345.f && y1[0] != 12345.f);\n  // errors: d = Y - target, (x, y) pairs in registers (v = 0, 1 and 2, 3)"),
+    ("  after_targets();\n  asm volatile(\"\" ::: \"memory\");                           // ... then the stores",
+     "  G2K_ST(42, " + PT + " && d0[0] != 12345.f && d1[3] != 12345.f);\n  after_targets();\n  asm volatile(\"\" ::: \"memory\");                           // ... then the stores"),
+    ("  float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f;",
+     "  G2K_ST(43, " + PT + ");\n  float ea = 0.f, eb = 0.f, ec = 0.f, el2 = 0.f;"),
+    ("  if (GRAD) {\n#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      d0[v] = has_t ? d0[v] : 0.f;",
+     "  G2K_ST(44, " + PT + " && acc[0] != 12345.f);\n  if (GRAD) {\n#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      d0[v] = has_t ? d0[v] : 0.f;"),
+]
+
+
+# every wave's own DMA wait before B1 (wave w -> slot 39 + w, w >= 1)
+TL_B1 = [
+    ("  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians",
+     "  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians\n  G2K_ST(112 + c.wv, true);"),
+    ("  // every kernel-argument line the prologue reads, in ONE scalar-load round",
+     "  G2K_ST(80 + (threadIdx.x >> 6), true);\n  // every kernel-argument line the prologue reads, in ONE scalar-load round"),
+    ("    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
+     "    G2K_ST(96 + c.wv, true);\n    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first"),
+    ("  __syncthreads();                                              // B1: window + weights landed",
+     "  G2K_ST(64 + c.wv, fb == 0);\n  __syncthreads();                                              // B1: window + weights landed"),
+]
+
+
+# position window by 1-KiB LDS-DMA instructions into unpadded rows
+POS1K = [
+    ("  s.pp = 2 * Nmax + 4;", "  s.pp = 2 * Nmax;"),
+    ("    if (wide) {\n      for (int i = 0; i < Nmax / 2; i += 64)\n        if (i + c.lane < Nmax / 2) dma16(g + 4 * (i + c.lane), d + 4 * i);\n    } else {",
+     "    if (wide) {\n      if (r == c.wv) dma_copy_n<NT>(src, c.sPos, wcc * Nmax / 2, c.wv, c.lane);\n    } else {"),
+]
+
+
+# minimal stamps: every wave's exit (slot 64 + wave), R0's start (0)
+TL_END = [
+    ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
+    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup',
+     '  G2K_ST(64 + c.wv, true);\n  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup'),
+]
+
+
+def tl_end_print(st, t):
+    import numpy as np
+    rel = (st - st[:, :1]) % (1 << 32)
+    ends = rel[:, 64:76]
+    na = t["n_active"].cpu().numpy()
+    print("wave exits (median over scenes, waves 0..11):", [int(x) for x in np.median(ends, axis=0)])
+    for lo, hi in ((0, 8), (8, 16), (16, 24), (24, 33)):
+        m = (na >= lo) & (na < hi)
+        if m.any():
+            e = ends[m]
+            print(f"  n_active in [{lo},{hi}): {int(m.sum())} scenes; recurrence exit {int(np.median(e[:, :4].max(1)))}, "
+                  f"producers exit {int(np.median(e[:, 4:].max(1)))}, max over these scenes: rec {int(e[:, :4].max())} prod {int(e[:, 4:].max())}")
 
 
 def tl_rec_print(st, t):
@@ -195,8 +257,13 @@ def tl_fwd_print(st, t):
               "  ".join(f"{v}:{rel[k]}" for k, v in names.items()))
         print("   items (poll start, poll end):", " ".join(f"({rel[13 + 2 * k]},{rel[14 + 2 * k]})" for k in range(6)))
         print("   recurrence frame ends:", " ".join(str(rel[30 + g]) for g in range(20)))
-    # medians over scenes
+    # the scenes that end last (realtime), with their two roles' ends
     rel = (st - st[:, :1]) % (1 << 32)
+    last = np.argsort(re)[-6:]
+    print("latest-ending scenes (scene, n_active, end tick, R0 stored, P0 published):",
+          [(int(k), int(t["n_active"][k]), int(re[k] - t0), int(rel[k][26]), int(rel[k][50])) for k in last])
+    print("end tick by n_active (mean):", {int(n): round(float((re - t0)[t["n_active"].cpu().numpy() == n].mean()), 1)
+                                          for n in sorted(set(t["n_active"].cpu().numpy().tolist()))[::4]})
     med = np.median(rel, axis=0)
     print("median:", "  ".join(f"{v}:{int(med[k])}" for k, v in names.items()))
     print("median recurrence frame ends:", " ".join(str(int(med[30 + g])) for g in range(20)))
@@ -224,6 +291,11 @@ VARIANTS = {
     "tl_fwd": {SCENE: TL_FWD},
     "tl_rec": {SCENE: TL_REC},
     "tl_lds": {SCENE: lds_stamps(TL_REC)},
+    "tl_tile": {SCENE: lds_stamps(TL_REC + TL_TILE)},
+    "tl_b1": {SCENE: lds_stamps(TL_B1 + TL_REC)},
+    "pos1k": {SCENE: POS1K},
+    "tl_end": {SCENE: lds_stamps(TL_END)},
+    "tl_b1_pos1k": {SCENE: lds_stamps(TL_B1 + TL_REC) + POS1K},
     "warm": {SCENE: WARM},
     "tl_lds_warm": {SCENE: lds_stamps(TL_REC) + WARM},
 }
@@ -234,11 +306,10 @@ def build_variant(name):
     tmp = tempfile.mkdtemp(prefix=f"g2k_{name}_")
     for f in os.listdir(src):
         shutil.copy(os.path.join(src, f), tmp)
-        if name == "orig" and f.endswith((".hip", ".h")):   # the committed sources
-            git = subprocess.run(["git", "-C", ROOT, "show", "HEAD:multimodaltraj_2_amd/csrc/" + f],
-                                 capture_output=True, text=True)
-            if git.returncode == 0:
-                open(os.path.join(tmp, f), "w").write(git.stdout)
+        if name == "orig":   # reference sources copied into tools/ab_ref (the box has no .git)
+            ref = os.path.join(ROOT, "tools", "ab_ref", f)
+            assert os.path.exists(ref), "tools/ab_ref is missing: copy a committed csrc there"
+            shutil.copy(ref, os.path.join(tmp, f))
     for fname, reps in VARIANTS[name].items():
         if fname == "__flags__":
             continue
@@ -310,8 +381,43 @@ def stamps(lib, c, t, dev, train=True):
         print("   heads (start, head done, flags):", " ".join(f"({rel[30 + 3 * i]},{rel[31 + 3 * i]},{rel[32 + 3 * i]})" for i in range(3)))
 
 
+def interleaved(cfg, names, rounds):
+    """Plain variants timed in interleaved rounds (A B A B ...): per variant the
+    median and min over rounds of the 200-launch HIP-event average."""
+    import numpy as np
+    c = dict(CONFIGS[cfg])
+    S = c["S"] if c["S"] <= 256 else c["S"] // 8
+    dev = torch.device("cuda")
+    t = make_batch(S, c["Nmax"], c["H"], seed=1).to_device(dev)
+    runs = {}
+    for name in names:
+        lib = _lib.load(build_variant(name))
+        _lib._lib = lib
+        params = fs.init_params(c["Nmax"], seed=0, device=dev)
+        plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+        tstep = ts.TrainStep(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+        runs[name] = (lib, plan, tstep)
+    res = {n: ([], []) for n in names}
+    for _ in range(rounds):
+        for name in names:
+            lib, plan, tstep = runs[name]
+            _lib._lib = lib
+            res[name][0].append(time_it(plan.run))
+            res[name][1].append(time_it(tstep.run))
+    for name in names:
+        f, tr = np.array(res[name][0]), np.array(res[name][1])
+        print(f"{cfg} {name:16s} fwd median {np.median(f):7.2f} min {f.min():7.2f}   "
+              f"train median {np.median(tr):7.2f} min {tr.min():7.2f}  ({rounds} rounds)", flush=True)
+
+
 def main():
     args = sys.argv[1:]
+    if args and args[0] == "--rounds":
+        rounds = int(args[1])
+        rest = args[2:]
+        cfg = rest[0] if rest and rest[0] in CONFIGS else "eth_hotel_synth"
+        interleaved(cfg, [a for a in rest if a in VARIANTS], rounds)
+        return
     cfg = args[0] if args and args[0] in CONFIGS else "eth_hotel_synth"
     names = [a for a in args if a in VARIANTS] or [v for v in VARIANTS if not v.startswith("stamps")]
     c = dict(CONFIGS[cfg])
@@ -330,16 +436,25 @@ def main():
             for _ in range(5):
                 plan.run()
             torch.cuda.synchronize()
-            buf = (ctypes.c_uint * (S * 64))()
-            assert lib.g2k_stamp_copy(buf, S * 64) == 0
-            st = np.frombuffer(buf, dtype=np.uint32).reshape(S, 64).astype(np.int64)
-            (tl_rec_print if name.startswith("tl_rec") or name.startswith("tl_lds") else tl_fwd_print)(st, t)
+            W = 128 if name in ("tl_lds", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end") else 64
+            buf = (ctypes.c_uint * (S * W))()
+            assert lib.g2k_stamp_copy(buf, S * W) == 0
+            st = np.frombuffer(buf, dtype=np.uint32).reshape(S, W).astype(np.int64)
+            {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print}.get(name, tl_rec_print)(st, t)
             print(f"{name}: fwd {time_it(plan.run):7.2f} us (stamped build)")
-            if name.startswith("tl_lds"):
+            if name in ("tl_lds", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k"):
                 rel = (st - st[:, :1]) % (1 << 32)
                 med = np.median(rel, axis=0)
                 print("head 0 (median): operands", int(med[60]), "A done", int(med[61]), "attn done",
                       int(med[62]))
+                if name.startswith("tl_b1"):
+                    print("B1 waits per wave (median, wave 0..11):", [int(med[64 + w]) for w in range(12)])
+                    print("wave starts (median, rel. to wave 0's stamp 0):", [int(med[80 + w]) for w in range(12)])
+                    print("wave DMA issue start (median):", [int(med[96 + w]) for w in range(12)])
+                    print("wave nact loaded (median):", [int(med[112 + w]) for w in range(12)])
+                if name == "tl_tile":
+                    print("last tile (median): entry", int(med[40]), "Y", int(med[41]), "targets", int(med[42]),
+                          "stores", int(med[43]), "errors", int(med[44]))
             continue
         if name.startswith("stamps"):
             lib.g2k_stamp_copy.argtypes = [ctypes.c_void_p, ctypes.c_int]
