@@ -47,9 +47,9 @@ constexpr int SM_SPARE = 1084;  // write-only word (stores of lanes without an e
 constexpr int kSceneSmall = 1088;
 constexpr int kKA = 12;       // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
 constexpr int kYP = 17;       // train: per-producer dY tile scratch [24][kYP] (pitch: bank spread)
-// per-worker tile scratch (floats): the prediction tile transposed for its
-// 16-byte stores ([28][16]: 24 pred rows + 4 rows that lanes without a row
-// write), then (train) the dY tile [24][kYP]
+// forward per-producer tile scratch (floats): the prediction tile transposed
+// for its 16-byte stores ([28][16]: 24 pred rows + 4 rows that lanes without
+// a row write); train keeps the dY tile [24][kYP] per worker
 constexpr int kYS = 448;
 constexpr int kTileStores = 8;   // global stores per prediction tile (4-byte path)
 // train mode
@@ -82,7 +82,8 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
   const int NG = NP + kRecW;                          // train: producers + recurrence waves
-  s.o_y = o;     o += (grad ? NG : (NP == 8 ? NP : 0)) * kYS;   // tile scratch (store transpose, dY)
+  // tile scratch: train, the dY tile per worker; forward NP = 8, the store transpose
+  s.o_y = o;     o += grad ? NG * kL2 * kYP : (NP == 8 ? NP * kYS : 0);
   s.o_met = o;   o += (grad ? NG : NP) * 8;
   s.o_ring = o;  o += fc * kD * kD;
   s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
@@ -1007,7 +1008,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
     load_targets(tgr, Nmax, c.nact, fb, f0, 0, f0 < fend, L, q, tg);
     balance_stores(a);
   }
-  float* ys = c.sY + slot * kYS;
+  float* ys = c.sY + slot * kL2 * kYP;
   f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   for (int fl = f0; fl < fend; fl += fstep) {
     const int f = fb + fl;
