@@ -350,6 +350,11 @@ __device__ __forceinline__ int sload_i32(const int32_t* p) {
   asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
   return v;
 }
+// two of them in one round trip
+__device__ __forceinline__ void sload2_i32(const int32_t* p, const int32_t* q, int& u, int& v) {
+  asm volatile("s_load_dword %0, %2, 0x0\n\ts_load_dword %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+               : "=&s"(u), "=&s"(v) : "s"(p), "s"(q) : "memory");
+}
 
 // Per-lane select written as bit operations (it compiles to v_cndmask_b32).
 // Left to itself the compiler turns a chain of ternaries on the lane index

@@ -60,8 +60,8 @@ constexpr int kGA_WC = 0, kGA_K1 = 192, kGA_VE = 272, kGA_BV = 304;
 
 struct SceneLayout {
   int fc, wcmax, pp;   // frames per chunk, window rows per chunk, pos row pitch (floats)
-  int o_wi, o_wo, o_vis, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_mflag, o_red, o_pos,
-      o_vg;
+  int o_wi, o_wo, o_vis, o_pm, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_mflag, o_red,
+      o_pos, o_vg;
   // train mode (zero-sized otherwise)
   int wtot;            // window rows of the whole scene ((F - 1) * stride + T)
   int dwo_seq;         // 1: dWo^T accumulated in frame order (one copy); 0: one copy per producer
@@ -79,6 +79,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_wi = o;    o += rup4(Nmax * kD);
   s.o_wo = o;    o += rup4(kT * Nmax);
   s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
+  s.o_pm = o;    o += rup4((Nmax + 3) / 4);            // the scene's ped_mask bytes (staged)
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
   const int NG = NP + kRecW;                          // train: producers + recurrence waves
@@ -303,6 +304,7 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
 struct SceneCtx {
   float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sPos, *sVG, *sY;
   float *sCost, *sGFrame, *sGPriv, *sGPdV, *sGAcc, *sGdV, *sGdWo;
+  const uint8_t* sPm;   // the scene's ped_mask bytes (when pm_staged)
   int* sFlag;     // As ring: global frame + 1 once the frame's As is in its slot
   int* sMflag;    // M ring: global frame + 1 once the frame's M is in its slot
   int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
@@ -932,9 +934,14 @@ __device__ __forceinline__ void grad_priv_sum(const SceneCtx& c, int NP) {
 // Pedestrian n = 16 t + L has targets (n < n_active and its ped_mask byte
 // set): bit t of the lane's word.  Read once per wave (a mask load inside the
 // tile loop would make the compiler wait for the targets prefetched behind it).
+__device__ __forceinline__ bool pm_staged(const StepArgs& a) {
+  return a.ped_mask != nullptr && (a.d.Nmax & 3) == 0 && (((uintptr_t)a.ped_mask) & 3) == 0;
+}
 __device__ __forceinline__ unsigned scene_act_bits(const StepArgs& a, const SceneCtx& c) {
   const int Nmax = a.d.Nmax;
-  const uint8_t* pm = a.ped_mask ? a.ped_mask + (size_t)c.s * Nmax : nullptr;
+  // the mask row was staged in LDS with the prologue's DMA (no dependent
+  // global byte loads here); else read from global memory
+  const uint8_t* pm = pm_staged(a) ? c.sPm : a.ped_mask ? a.ped_mask + (size_t)c.s * Nmax : nullptr;
   bool on[kMaxN / 64];
 #pragma unroll
   for (int j = 0; j < kMaxN / 64; ++j) {
@@ -1093,7 +1100,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
   const int pw = c.wv - kRecW, L = c.L, q = c.q, lane = c.lane, s = c.s, ntact = c.ntact;
-  const unsigned act_bits = scene_act_bits(a, c);
+  unsigned act_bits = 0;   // after the first chunk's B1 (the staged mask has landed)
   // tile items of a chunk (forward): item j -> frame j / ntact, tile
   // j % ntact; this producer takes items pw, pw + NP, ...  (GRAD: whole
   // frames per worker, grad_frames)
@@ -1119,6 +1126,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
     scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});
+    if (fb == 0) act_bits = scene_act_bits(a, c);
     const int nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;   // forward
     // GRAD: this producer's frames pw, pw + NP, ... < gend of the chunk (the
     // last R frames of the last chunk go to the recurrence waves)
@@ -1344,6 +1352,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.sm = smem + lay.o_small; c.sMet = smem + lay.o_met; c.sRing = smem + lay.o_ring;
   c.sMring = smem + lay.o_mring; c.sRed = smem + lay.o_red; c.sPos = smem + lay.o_pos;
   c.sVG = smem + lay.o_vg;
+  c.sPm = reinterpret_cast<const uint8_t*>(smem + lay.o_pm);
   c.sFlag = reinterpret_cast<int*>(smem + lay.o_flag);
   c.sMflag = reinterpret_cast<int*>(smem + lay.o_mflag);
   c.sY = smem + lay.o_y;
@@ -1365,6 +1374,10 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
     // the small segments: one wave each (one pointer per wave keeps the
     // kernel-argument loads off a serial s_load / s_waitcnt chain)
+    if (pm_staged(a) && wv == 10 % (NT / 64) && lane < Nmax / 4)   // the ped_mask row, 4 bytes a lane
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(a.ped_mask + (size_t)c.s * Nmax + 4 * lane),
+          (__attribute__((address_space(3))) void*)(smem + lay.o_pm), 4, 0, 0);
     for (int seg = wv; seg < 10; seg += NT / 64) {
       const float* src;
       float* dst;
@@ -1399,8 +1412,12 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
       c.sMflag[c.tid] = 0;
     }
   }
-  c.nact = clampi(sload_i32(a.n_active + c.s), 0, Nmax);
-  c.nf = a.n_frames ? clampi(sload_i32(a.n_frames + c.s), 0, F) : F;
+  {
+    int na, nf;
+    sload2_i32(a.n_active + c.s, a.n_frames ? a.n_frames + c.s : a.n_active + c.s, na, nf);
+    c.nact = clampi(na, 0, Nmax);
+    c.nf = a.n_frames ? clampi(nf, 0, F) : F;
+  }
   c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians
   if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
   if (c.wv < kRecW) {

@@ -133,7 +133,7 @@ __shared__ unsigned g2k_lds_stamp[128];
 HEAD_ST = "__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 4 && wrow0 == 0"
 
 
-def lds_stamps(reps):
+def lds_stamps(reps, head=True):
     out = []
     for a, b in reps:
         b = b.replace(STAMP_DEF, LDS_STAMP_DEF)
@@ -144,6 +144,9 @@ def lds_stamps(reps):
         ('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup',
          '  __syncthreads();\n  if (c.tid < 128) g2k_stamp_buf[(size_t)c.s * 128 + c.tid] = g2k_lds_stamp[c.tid];\n'
          '  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup'),
+    ]
+    if head:
+        out += [
         ("  f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);",
          "  G2K_ST(60, " + HEAD_ST + ");\n  f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);"),
         ("  __builtin_amdgcn_sched_barrier(0);\n  attn_weights(aA, as_dst, L, q);",
@@ -217,6 +220,8 @@ TL_END = [
 def tl_end_print(st, t):
     import numpy as np
     rel = (st - st[:, :1]) % (1 << 32)
+    print("WG duration (wave 0 start -> last wave exit, cycles): median", int(np.median(rel[:, 64:76].max(1))),
+          "max", int(rel[:, 64:76].max()))
     ends = rel[:, 64:76]
     na = t["n_active"].cpu().numpy()
     print("wave exits (median over scenes, waves 0..11):", [int(x) for x in np.median(ends, axis=0)])
@@ -294,7 +299,8 @@ VARIANTS = {
     "tl_tile": {SCENE: lds_stamps(TL_REC + TL_TILE)},
     "tl_b1": {SCENE: lds_stamps(TL_B1 + TL_REC)},
     "pos1k": {SCENE: POS1K},
-    "tl_end": {SCENE: lds_stamps(TL_END)},
+    "tl_end": {SCENE: lds_stamps(TL_END, head=False)},
+    "tl_end_orig": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_b1_pos1k": {SCENE: lds_stamps(TL_B1 + TL_REC) + POS1K},
     "warm": {SCENE: WARM},
     "tl_lds_warm": {SCENE: lds_stamps(TL_REC) + WARM},
@@ -306,7 +312,7 @@ def build_variant(name):
     tmp = tempfile.mkdtemp(prefix=f"g2k_{name}_")
     for f in os.listdir(src):
         shutil.copy(os.path.join(src, f), tmp)
-        if name == "orig":   # reference sources copied into tools/ab_ref (the box has no .git)
+        if name == "orig" or name.endswith("_orig"):   # reference sources in tools/ab_ref (no .git on the box)
             ref = os.path.join(ROOT, "tools", "ab_ref", f)
             assert os.path.exists(ref), "tools/ab_ref is missing: copy a committed csrc there"
             shutil.copy(ref, os.path.join(tmp, f))
@@ -389,20 +395,26 @@ def interleaved(cfg, names, rounds):
     S = c["S"] if c["S"] <= 256 else c["S"] // 8
     dev = torch.device("cuda")
     t = make_batch(S, c["Nmax"], c["H"], seed=1).to_device(dev)
+    # as bench.py: n_frames and ped_mask bound; AB_ROTATE=K input batches in
+    # rotation (no Infinity Cache hits), K = 1 by default
+    K = int(os.environ.get("AB_ROTATE", "1"))
+    batches = [t] + [make_batch(S, c["Nmax"], c["H"], seed=100 + k).to_device(dev) for k in range(1, K)]
     runs = {}
     for name in names:
         lib = _lib.load(build_variant(name))
         _lib._lib = lib
         params = fs.init_params(c["Nmax"], seed=0, device=dev)
-        plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+        plans = [fs.StepPlan(params, b["pos"], b["vislet"], b["G"], b["targets"], b["n_active"], b["h0"],
+                             n_frames=b["n_frames"], ped_mask=b["ped_mask"]) for b in batches]
         tstep = ts.TrainStep(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
-        runs[name] = (lib, plan, tstep)
+        it = iter(range(1 << 62))
+        runs[name] = (lib, (lambda ps=plans, it=it: ps[next(it) % len(ps)].run()), tstep)
     res = {n: ([], []) for n in names}
     for _ in range(rounds):
         for name in names:
-            lib, plan, tstep = runs[name]
+            lib, run, tstep = runs[name]
             _lib._lib = lib
-            res[name][0].append(time_it(plan.run))
+            res[name][0].append(time_it(run))
             res[name][1].append(time_it(tstep.run))
     for name in names:
         f, tr = np.array(res[name][0]), np.array(res[name][1])
@@ -432,15 +444,29 @@ def main():
             import numpy as np
             lib.g2k_stamp_copy.argtypes = [ctypes.c_void_p, ctypes.c_int]
             params = fs.init_params(c["Nmax"], seed=0, device=dev)
-            plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
-            for _ in range(5):
-                plan.run()
+            # AB_ROTATE=K: the stamped launch reads inputs none of the K-1
+            # launches before it touched (no Infinity Cache hits), as bench.py
+            K = int(os.environ.get("AB_ROTATE", "0"))
+            if K:
+                plans = []
+                for k in range(K):
+                    tk = t if k == K - 1 else make_batch(S, c["Nmax"], c["H"], seed=100 + k).to_device(dev)
+                    plans.append(fs.StepPlan(params, tk["pos"], tk["vislet"], tk["G"], tk["targets"],
+                                             tk["n_active"], tk["h0"], n_frames=tk["n_frames"],
+                                             ped_mask=tk["ped_mask"]))
+                for p_ in plans:
+                    p_.run()
+                plan = plans[-1]
+            else:
+                plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+                for _ in range(5):
+                    plan.run()
             torch.cuda.synchronize()
-            W = 128 if name in ("tl_lds", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end") else 64
+            W = 128 if name in ("tl_lds", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig") else 64
             buf = (ctypes.c_uint * (S * W))()
             assert lib.g2k_stamp_copy(buf, S * W) == 0
             st = np.frombuffer(buf, dtype=np.uint32).reshape(S, W).astype(np.int64)
-            {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print}.get(name, tl_rec_print)(st, t)
+            {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print, "tl_end_orig": tl_end_print}.get(name, tl_rec_print)(st, t)
             print(f"{name}: fwd {time_it(plan.run):7.2f} us (stamped build)")
             if name in ("tl_lds", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k"):
                 rel = (st - st[:, :1]) % (1 << 32)
