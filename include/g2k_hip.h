@@ -101,8 +101,9 @@ int64_t g2k_step_workspace_bytes(const g2k_dims* d);
  *   h_in     [S, D, H]             hidden_state entering frame 0
  *   h_out    [S, D, H]             hidden_state after the last frame (may alias h_in)
  *   pred     [S, F, 2L, Nmax]      pred_path_band per frame (rows x then y); only
- *                                  frames < n_frames and columns < n_active (in
- *                                  groups of 4, the extra columns 0) are written
+ *                                  frames < n_frames and columns < min(Nmax,
+ *                                  16 ceil(n_active / 16)) are written (whole
+ *                                  16-column tiles: the columns past n_active 0)
  *   metrics  [S, 8]                {sum ade_spec, count, sum |fde|^2,
  *                                   sum ade_l2, sum |fde|, frames, 0, 0}
  *   A_out    [S, F, D, D] or NULL  krnl_mdl.attn per frame (frames < n_frames)

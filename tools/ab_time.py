@@ -299,6 +299,7 @@ VARIANTS = {
     "tl_tile": {SCENE: lds_stamps(TL_REC + TL_TILE)},
     "tl_b1": {SCENE: lds_stamps(TL_B1 + TL_REC)},
     "pos1k": {SCENE: POS1K},
+    "fullseg": {SCENE: [("    const bool okc = n0 + c4 < nact;", "    const bool okc = n0 + c4 < Nmax;")]},
     "tl_end": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_end_orig": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_b1_pos1k": {SCENE: lds_stamps(TL_B1 + TL_REC) + POS1K},
