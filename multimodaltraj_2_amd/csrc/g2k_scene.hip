@@ -60,7 +60,7 @@ constexpr int kGA_WC = 0, kGA_K1 = 192, kGA_VE = 272, kGA_BV = 304;
 
 struct SceneLayout {
   int fc, wcmax, pp;   // frames per chunk, window rows per chunk, pos row pitch (floats)
-  int o_wi, o_wo, o_vis, o_pm, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_mflag, o_red,
+  int o_wi, o_wo, o_vis, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_mflag, o_red,
       o_pos, o_vg;
   // train mode (zero-sized otherwise)
   int wtot;            // window rows of the whole scene ((F - 1) * stride + T)
@@ -79,7 +79,6 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_wi = o;    o += rup4(Nmax * kD);
   s.o_wo = o;    o += rup4(kT * Nmax);
   s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
-  s.o_pm = o;    o += rup4((Nmax + 3) / 4);            // the scene's ped_mask bytes (staged)
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
   const int NG = NP + kRecW;                          // train: producers + recurrence waves
@@ -304,7 +303,6 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
 struct SceneCtx {
   float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sPos, *sVG, *sY;
   float *sCost, *sGFrame, *sGPriv, *sGPdV, *sGAcc, *sGdV, *sGdWo;
-  const uint8_t* sPm;   // the scene's ped_mask bytes (when pm_staged)
   int* sFlag;     // As ring: global frame + 1 once the frame's As is in its slot
   int* sMflag;    // M ring: global frame + 1 once the frame's M is in its slot
   int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
@@ -936,28 +934,38 @@ __device__ __forceinline__ void grad_priv_sum(const SceneCtx& c, int NP) {
 }
 
 // Pedestrian n = 16 t + L has targets (n < n_active and its ped_mask byte
-// set): bit t of the lane's word.  Read once per wave (a mask load inside the
-// tile loop would make the compiler wait for the targets prefetched behind it).
-__device__ __forceinline__ bool pm_staged(const StepArgs& a) {
-  return a.ped_mask != nullptr && (a.d.Nmax & 3) == 0 && (((uintptr_t)a.ped_mask) & 3) == 0;
-}
+// set): bit t of the lane's word.  The mask row is read as one dword per lane
+// (pedestrians 4l .. 4l + 3 in lane l) and spread by four ballots: one
+// global round trip per wave, not one per 64 pedestrians (each was a
+// dependent byte load; a mask load inside the tile loop would also make the
+// compiler wait for the targets prefetched behind it).
 __device__ __forceinline__ unsigned scene_act_bits(const StepArgs& a, const SceneCtx& c) {
   const int Nmax = a.d.Nmax;
-  // the mask row was staged in LDS with the prologue's DMA (no dependent
-  // global byte loads here); else read from global memory
-  const uint8_t* pm = pm_staged(a) ? c.sPm : a.ped_mask ? a.ped_mask + (size_t)c.s * Nmax : nullptr;
-  bool on[kMaxN / 64];
+  unsigned long long B[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // bit l: pedestrian 4 l + b has a target
+  if (a.ped_mask) {
+    const uint8_t* pm = a.ped_mask + (size_t)c.s * Nmax;
+    uint32_t w = 0;
+    if ((Nmax & 3) == 0 && (((uintptr_t)a.ped_mask) & 3) == 0) {
+      const int l = c.lane < Nmax / 4 ? c.lane : 0;
+      w = reinterpret_cast<const uint32_t*>(pm)[l];
+    } else {
 #pragma unroll
-  for (int j = 0; j < kMaxN / 64; ++j) {
-    const int n = c.lane + 64 * j;
-    on[j] = n < c.nact && (pm ? pm[n < Nmax ? n : 0] != 0 : true);
+      for (int b = 0; b < 4; ++b) {
+        const int n = 4 * c.lane + b;
+        w |= (uint32_t)(n < Nmax ? pm[n] : 0) << (8 * b);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) B[b] = __builtin_amdgcn_ballot_w64(((w >> (8 * b)) & 0xffu) != 0);
   }
+  const int b = c.L & 3;
+  const unsigned long long mine = b == 0 ? B[0] : b == 1 ? B[1] : b == 2 ? B[2] : B[3];
   unsigned bits = 0;
 #pragma unroll
-  for (int j = 0; j < kMaxN / 64; ++j) {
-    const unsigned long long b = __builtin_amdgcn_ballot_w64(on[j]);
-#pragma unroll
-    for (int tt = 0; tt < 4; ++tt) bits |= (unsigned)((b >> (16 * tt + c.L)) & 1ull) << (4 * j + tt);
+  for (int t = 0; t < kMaxN / 16; ++t) {
+    const int n = 16 * t + c.L;
+    const unsigned on = (unsigned)((mine >> (4 * t + (c.L >> 2))) & 1ull);
+    bits |= (n < c.nact ? on : 0u) << t;
   }
   return bits;
 }
@@ -1104,7 +1112,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
   const int pw = c.wv - kRecW, L = c.L, q = c.q, lane = c.lane, s = c.s, ntact = c.ntact;
-  unsigned act_bits = 0;   // after the first chunk's B1 (the staged mask has landed)
+  const unsigned act_bits = scene_act_bits(a, c);
   // tile items of a chunk (forward): item j -> frame j / ntact, tile
   // j % ntact; this producer takes items pw, pw + NP, ...  (GRAD: whole
   // frames per worker, grad_frames)
@@ -1130,7 +1138,6 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
     scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});
-    if (fb == 0) act_bits = scene_act_bits(a, c);
     const int nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;   // forward
     // GRAD: this producer's frames pw, pw + NP, ... < gend of the chunk (the
     // last R frames of the last chunk go to the recurrence waves)
@@ -1356,7 +1363,6 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.sm = smem + lay.o_small; c.sMet = smem + lay.o_met; c.sRing = smem + lay.o_ring;
   c.sMring = smem + lay.o_mring; c.sRed = smem + lay.o_red; c.sPos = smem + lay.o_pos;
   c.sVG = smem + lay.o_vg;
-  c.sPm = reinterpret_cast<const uint8_t*>(smem + lay.o_pm);
   c.sFlag = reinterpret_cast<int*>(smem + lay.o_flag);
   c.sMflag = reinterpret_cast<int*>(smem + lay.o_mflag);
   c.sY = smem + lay.o_y;
@@ -1378,10 +1384,6 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
     // the small segments: one wave each (one pointer per wave keeps the
     // kernel-argument loads off a serial s_load / s_waitcnt chain)
-    if (pm_staged(a) && wv == 10 % (NT / 64) && lane < Nmax / 4)   // the ped_mask row, 4 bytes a lane
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(a.ped_mask + (size_t)c.s * Nmax + 4 * lane),
-          (__attribute__((address_space(3))) void*)(smem + lay.o_pm), 4, 0, 0);
     for (int seg = wv; seg < 10; seg += NT / 64) {
       const float* src;
       float* dst;
