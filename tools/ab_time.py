@@ -300,6 +300,21 @@ VARIANTS = {
     "tl_b1": {SCENE: lds_stamps(TL_B1 + TL_REC)},
     "pos1k": {SCENE: POS1K},
     "fullseg": {SCENE: [("    const bool okc = n0 + c4 < nact;", "    const bool okc = n0 + c4 < Nmax;")]},
+    "zerotail": {SCENE: [("          load_item(fb, nitems, k + 3, tgB);\n        }\n      }\n    }\n",
+        "          load_item(fb, nitems, k + 3, tgB);\n        }\n      }\n"
+        "      if ((Nmax & 3) == 0) {\n"
+        "        const int nz = c.ntiles - ntact;\n"
+        "        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);\n"
+        "        const int row = lane >> 2, c4 = 4 * (lane & 3);\n"
+        "        for (int j = pw; j < cnt * nz; j += NP) {\n"
+        "          const int fl = j / nz, t = ntact + (j - fl * nz), n0 = 16 * t;\n"
+        "          const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + fb + fl) * kL2 * Nmax : a.targets,\n"
+        "                                      a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);\n"
+        "          bstore4(pr, n0 + c4 < Nmax ? (row * Nmax + n0 + c4) * 4 : kBufOff, z4);\n"
+        "          bstore4(pr, (n0 + c4 < Nmax && lane < 32) ? ((16 + row) * Nmax + n0 + c4) * 4 : kBufOff, z4);\n"
+        "        }\n"
+        "      }\n"
+        "    }\n")]},
     "tl_end": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_end_orig": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_b1_pos1k": {SCENE: lds_stamps(TL_B1 + TL_REC) + POS1K},
