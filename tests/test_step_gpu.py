@@ -100,6 +100,28 @@ def test_step_nonzero_h0_and_masks(gpu):
         assert close(met[s, :6], m[:6]) <= TOL
 
 
+@pytest.mark.parametrize("Nmax", [30, 64])
+def test_step_masks_byte_and_dword_rows(gpu, Nmax):
+    """ped_mask rows read per byte (Nmax % 4 != 0) and per dword (ballot
+    spread), with pedestrians masked at every residue mod 4 and past a tile
+    boundary; columns of the written tiles past n_active are 0."""
+    S = 3
+    mask = np.ones((S, Nmax), bool)
+    mask[0, 1::4] = False
+    mask[1, 2::5] = False
+    mask[2, 16:20] = False
+    b, out, res = run_both(S, Nmax, 128, ped_mask=mask, n_frames=[20, 13, 20], device=gpu)
+    met = out.metrics.cpu().numpy()
+    pred = out.pred.cpu().numpy()
+    for s in range(S):
+        pr, h, m, ex = res[s]
+        n = int(b.n_active[s])
+        nf = pr.shape[0]
+        assert close(pred[s, :nf, :, :n].reshape(nf, 2, 12, n), pr) <= TOL
+        assert np.all(pred[s, :, :, n:] == 0)
+        assert close(met[s, :6], m[:6]) <= TOL
+
+
 def test_step_deterministic(gpu):
     b = make_batch(8, 32, 128, seed=5)
     params = fs.init_params(32, seed=0, device=gpu)

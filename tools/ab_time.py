@@ -315,6 +315,9 @@ VARIANTS = {
         "        }\n"
         "      }\n"
         "    }\n")]},
+    "recprio1": {SCENE: [("      __builtin_amdgcn_s_setprio(2);\n      const float* as_lane", "      __builtin_amdgcn_s_setprio(1);\n      const float* as_lane")]},
+    "recprio3": {SCENE: [("      __builtin_amdgcn_s_setprio(2);\n      const float* as_lane", "      __builtin_amdgcn_s_setprio(3);\n      const float* as_lane")]},
+    "headprio": {SCENE: [("      if (fl < kRecW) __builtin_amdgcn_s_setprio(1);", "      __builtin_amdgcn_s_setprio(1);")]},
     "tl_end": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_end_orig": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_b1_pos1k": {SCENE: lds_stamps(TL_B1 + TL_REC) + POS1K},
