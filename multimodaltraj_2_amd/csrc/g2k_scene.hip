@@ -47,10 +47,6 @@ constexpr int SM_SPARE = 1084;  // write-only word (stores of lanes without an e
 constexpr int kSceneSmall = 1088;
 constexpr int kKA = 12;       // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
 constexpr int kYP = 17;       // train: per-producer dY tile scratch [24][kYP] (pitch: bank spread)
-// forward per-producer tile scratch (floats): the prediction tile transposed
-// for its 16-byte stores ([28][16]: 24 pred rows + 4 rows that lanes without
-// a row write); train keeps the dY tile [24][kYP] per worker
-constexpr int kYS = 448;
 constexpr int kTileStores = 8;   // global stores per prediction tile (4-byte path)
 // train mode
 constexpr int kGFrame = 192;  // per-producer frame scratch: dM [24][8] (frame_grad's P6)
@@ -82,8 +78,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
   const int NG = NP + kRecW;                          // train: producers + recurrence waves
-  // tile scratch: train, the dY tile per worker; forward NP = 8, the store transpose
-  s.o_y = o;     o += grad ? NG * kL2 * kYP : (NP == 8 ? NP * kYS : 0);
+  s.o_y = o;     o += grad ? NG * kL2 * kYP : 0;      // dY tile scratch (train)
   s.o_met = o;   o += (grad ? NG : NP) * 8;
   s.o_ring = o;  o += fc * kD * kD;
   s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
@@ -582,7 +577,7 @@ __device__ __forceinline__ int mrow(int r) { return (r & 1) * kL + (r >> 1); }
 // `after_targets` runs once the target registers are consumed (GRAD: the
 // next tile's targets are loaded into them there, before this tile's stores,
 // so the next tile's wait counts exactly those stores).
-template <bool GRAD, bool TS, typename AfterTargets>
+template <bool GRAD, typename AfterTargets>
 __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, brsrc pr,
                                           const float2 (&tg)[4], bool has_t, int Nmax, int nact,
                                           int t, int L, int q, float acc[5], float& lsum,
@@ -620,31 +615,13 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
   }
   after_targets();
   asm volatile("" ::: "memory");                           // ... then the stores
-  if (TS && (Nmax & 3) == 0) {
-    // the tile transposed through the wave's scratch (physical pred rows x
-    // 16 columns) so that a lane stores four consecutive pedestrians of one
-    // row: two 16-byte stores per lane instead of eight 4-byte ones (the
-    // CU's vector-memory issue is what the producers queue on).  The tile's
-    // 16 columns are written whole (Y = 0 past n_active, w = 0 there): a
-    // 64-byte segment per row, where a partial one costs the memory side a
-    // read-modify-write once the output is not cache-resident (measured
-    // with rotated outputs: 21.5 -> 20.8 us per step at eth_hotel_synth).
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      ys[mrow(4 * q + v) * 16 + L] = y0[v];
-      ys[(hi ? mrow(16 + 4 * q + v) : kL2 + v) * 16 + L] = y1[v];   // rows 24..27: unused
-    }
-    wave_lds_sync();
-    const int lane = L + 16 * q, row = lane >> 2, c4 = 4 * (lane & 3);
-    const float4 s0 = *reinterpret_cast<const float4*>(ys + row * 16 + c4);              // rows 0..15
-    const float4 s1 = *reinterpret_cast<const float4*>(ys + (16 + (row & 7)) * 16 + c4);  // 16..23
-    const bool okc = n0 + c4 < Nmax;
-    bstore4(pr, okc ? (row * Nmax + n0 + c4) * 4 : kBufOff, s0);
-    bstore4(pr, (okc && lane < 32) ? ((16 + row) * Nmax + n0 + c4) * 4 : kBufOff, s1);
-  } else {
+  {
     // range-checked 4-byte stores (no branch): the block-1 rows of lane
-    // groups 2, 3 and columns past Nmax fall outside the frame's buffer; the
-    // tile's columns past n_active are written too (Y = 0), see above
+    // groups 2, 3 and columns past Nmax fall outside the frame's buffer.  The
+    // tile's 16 columns are written whole (Y = 0 past n_active, w = 0 there):
+    // 64-byte row segments, where a partial one costs the memory side a
+    // read-modify-write once the output is not cache-resident (rotated
+    // outputs: 21.5 -> 20.7 us per step at eth_hotel_synth)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       bstore(pr, n < Nmax ? (mrow(4 * q + v) * Nmax + n) * 4 : kBufOff, y0[v]);
@@ -1038,7 +1015,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
       const bool nxt = t + 1 < ntact;                    // the next tile: this frame's, else the next frame's
       const int nfl = nxt ? fl : fl + fstep, nt = nxt ? t + 1 : 0;
       f32x4 dWoT;
-      pred_tile<true, false>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
+      pred_tile<true>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
                       c.nact, t, L, q, acc, lsum, dm, dWoT,
                       [&] { load_targets(tgr, Nmax, c.nact, fb, nfl, nt, nfl < fend, L, q, tg); });
       // dWo^T[n0 + 4q + v][t = L]: one copy per worker, or one copy added
@@ -1203,7 +1180,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
         const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : a.targets,
                                     a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
         f32x4 dWoT;
-        pred_tile<false, NP == 8>(c.sMring + fl * kL2 * kT, c.sWo, c.sY + pw * kYS, pr, tg, (act_bits >> t) & 1u, Nmax,
+        pred_tile<false>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tg, (act_bits >> t) & 1u, Nmax,
                          c.nact, t, L, q, acc, lsum, dm, dWoT, [] {});
       };
       for (int k = 0; k < nitems; k += 2) {
@@ -1435,17 +1412,18 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
 }
 
 // Fused scene kernel geometry: producer waves (NP).  Measured (round 1,
-// 400 steps): eth_hotel_synth (H 128, Nmax 32) NP 8 19.9 us vs NP 12 20.2,
-// NP 6 22.2, NP 4 24.3; H 256 / Nmax 64: NP 12 28.2 vs NP 8 29.6; dense
-// crowd (H 256, Nmax 256): NP 12 53.2 vs NP 8 60.5; k-fold (H 128, Nmax 64):
-// NP 12 23.6 vs NP 8 25.4.  So 12 producers (16 waves, 4 per SIMD) once
-// H >= 256 or Nmax >= 64, else 8; H = 512 needs > 128 VGPRs per wave: 4.
-// Train mode keeps 8 (its producers need more than the 128 VGPRs per wave
-// that 16 waves leave).
+// 400 steps): H 256 / Nmax 64: NP 12 28.2 us vs NP 8 29.6; dense crowd
+// (H 256, Nmax 256): NP 12 53.2 vs NP 8 60.5; k-fold (H 128, Nmax 64): NP 12
+// 23.6 vs NP 8 25.4; eth_hotel_synth (H 128, Nmax 32) then favoured NP 8
+// (19.9 vs 20.2), but with this round's cheaper tiles its two-tile scenes are
+// producer-bound: NP 12 19.98 vs NP 8 20.75 us (rotated inputs).  So 12
+// producers (16 waves, 4 per SIMD) for the forward; H = 512 needs > 128
+// VGPRs per wave: 4.  Train mode keeps 8 (its producers need more than the
+// 128 VGPRs per wave that 16 waves leave).
 int scene_producers(int H, int Nmax, bool grad) {
+  (void)Nmax;
   if (H >= 512) return 4;
-  if (grad) return 8;
-  return (H >= 256 || Nmax >= 64) ? 12 : 8;
+  return grad ? 8 : 12;
 }
 
 template <int TPW, int NP, bool GRAD>
@@ -1457,19 +1435,23 @@ void launch_k(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
 template <bool GRAD>
 int launch_np(const StepArgs& a, const SceneLayout& l, int NP, int tpw, hipStream_t st) {
   if (NP == 4 && tpw == 8) { launch_k<8, 4, GRAD>(a, l, st); return G2K_OK; }
-  if (NP == 8) {
-    switch (tpw) {
-      case 1: launch_k<1, 8, GRAD>(a, l, st); return G2K_OK;
-      case 2: launch_k<2, 8, GRAD>(a, l, st); return G2K_OK;
-      case 4: launch_k<4, 8, GRAD>(a, l, st); return G2K_OK;
-      default: break;
+  if constexpr (GRAD) {   // train: NP = 8; forward: NP = 12 (scene_producers)
+    if (NP == 8) {
+      switch (tpw) {
+        case 1: launch_k<1, 8, true>(a, l, st); return G2K_OK;
+        case 2: launch_k<2, 8, true>(a, l, st); return G2K_OK;
+        case 4: launch_k<4, 8, true>(a, l, st); return G2K_OK;
+        default: break;
+      }
     }
-  } else if (NP == 12 && !GRAD) {
-    switch (tpw) {
-      case 1: launch_k<1, 12, false>(a, l, st); return G2K_OK;
-      case 2: launch_k<2, 12, false>(a, l, st); return G2K_OK;
-      case 4: launch_k<4, 12, false>(a, l, st); return G2K_OK;
-      default: break;
+  } else {
+    if (NP == 12) {
+      switch (tpw) {
+        case 1: launch_k<1, 12, false>(a, l, st); return G2K_OK;
+        case 2: launch_k<2, 12, false>(a, l, st); return G2K_OK;
+        case 4: launch_k<4, 12, false>(a, l, st); return G2K_OK;
+        default: break;
+      }
     }
   }
   return set_err(G2K_EUNSUPPORTED, "scene kernel not built for H=%d (NP=%d)", a.d.H, NP);

@@ -318,6 +318,10 @@ VARIANTS = {
     "recprio1": {SCENE: [("      __builtin_amdgcn_s_setprio(2);\n      const float* as_lane", "      __builtin_amdgcn_s_setprio(1);\n      const float* as_lane")]},
     "recprio3": {SCENE: [("      __builtin_amdgcn_s_setprio(2);\n      const float* as_lane", "      __builtin_amdgcn_s_setprio(3);\n      const float* as_lane")]},
     "headprio": {SCENE: [("      if (fl < kRecW) __builtin_amdgcn_s_setprio(1);", "      __builtin_amdgcn_s_setprio(1);")]},
+    "np12": {SCENE: [("  return (H >= 256 || Nmax >= 64) ? 12 : 8;", "  return 12;")]},
+    "np12ts": {SCENE: [("  return (H >= 256 || Nmax >= 64) ? 12 : 8;", "  return 12;"),
+                       ("pred_tile<false, NP == 8>", "pred_tile<false, true>"),
+                       ("o += grad ? NG * kL2 * kYP : (NP == 8 ? NP * kYS : 0);", "o += grad ? NG * kL2 * kYP : NP * kYS;")]},
     "tl_end": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_end_orig": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_b1_pos1k": {SCENE: lds_stamps(TL_B1 + TL_REC) + POS1K},
