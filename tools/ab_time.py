@@ -322,6 +322,8 @@ VARIANTS = {
     "np12ts": {SCENE: [("  return (H >= 256 || Nmax >= 64) ? 12 : 8;", "  return 12;"),
                        ("pred_tile<false, NP == 8>", "pred_tile<false, true>"),
                        ("o += grad ? NG * kL2 * kYP : (NP == 8 ? NP * kYS : 0);", "o += grad ? NG * kL2 * kYP : NP * kYS;")]},
+    "lateloads": {SCENE: [("    } else {\n      load_item(fb, nitems, 0, tgA);\n      load_item(fb, nitems, 1, tgB);\n    }\n", "    }\n"),
+                          ("      for (int k = 0; k < nitems; k += 2) {", "      load_item(fb, nitems, 0, tgA);\n      load_item(fb, nitems, 1, tgB);\n      for (int k = 0; k < nitems; k += 2) {")]},
     "tl_end": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_end_orig": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_b1_pos1k": {SCENE: lds_stamps(TL_B1 + TL_REC) + POS1K},
