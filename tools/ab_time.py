@@ -324,6 +324,7 @@ VARIANTS = {
                        ("o += grad ? NG * kL2 * kYP : (NP == 8 ? NP * kYS : 0);", "o += grad ? NG * kL2 * kYP : NP * kYS;")]},
     "lateloads": {SCENE: [("    } else {\n      load_item(fb, nitems, 0, tgA);\n      load_item(fb, nitems, 1, tgB);\n    }\n", "    }\n"),
                           ("      for (int k = 0; k < nitems; k += 2) {", "      load_item(fb, nitems, 0, tgA);\n      load_item(fb, nitems, 1, tgB);\n      for (int k = 0; k < nitems; k += 2) {")]},
+    "prodsleep": {SCENE: [("        item(k, tgA);\n", "        item(k, tgA);\n        __builtin_amdgcn_s_sleep(2);\n")]},
     "tl_end": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_end_orig": {SCENE: lds_stamps(TL_END, head=False)},
     "tl_b1_pos1k": {SCENE: lds_stamps(TL_B1 + TL_REC) + POS1K},
