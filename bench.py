@@ -214,6 +214,28 @@ def load_pmc(name):
         return None
 
 
+def real_scene_batch(S, H, rank, world):
+    """Config 3's workload on real data: the k-fold-4 training datasets plus
+    ETH hotel (multimodaltraj_2_amd/realdata.py: distinct sample.py scenes,
+    natively planned), S per rank, rank r taking the r-th contiguous shard of
+    the S * world global scenes.  Data: the reference's CSV arrays committed
+    under tests/golden/ (the bench's input files; the product reads a data
+    root)."""
+    from multimodaltraj_2_amd import realdata as rd
+    from multimodaltraj_2_amd.synthetic import SceneBatch
+    from multimodaltraj_2_amd.train import plan_subset
+    raw = {n: np.load(os.path.join(ROOT, "tests", "golden", f"data_{n}.npz"))["raw_data"]
+           for n in rd.fold_datasets(4)}
+    plan = rd.plan_scenes(S * world, raw)
+    sub = plan_subset(plan, np.arange(rank * S, (rank + 1) * S))
+    h = sub.host()
+    rng = np.random.default_rng(1 + rank)
+    return SceneBatch(pos=h["pos"], vislet=h["vislet"],
+                      G=rng.standard_normal((S, 16, 8)).astype(np.float32), targets=h["targets"],
+                      n_active=h["n_active"], h0=np.zeros((S, 16, H), np.float32), stride=0,
+                      n_frames=h["n_frames"], ped_mask=h["ped_mask"])
+
+
 def selftest_worker(args, world, rank):
     """--selftest-launcher (CPU, gloo): the launcher, the process-group check,
     the timing brackets and the metric all-reduce, with a no-op step in place
@@ -263,10 +285,8 @@ def main(argv=None):
         return selftest_worker(args, world, rank)
 
     if args.config == REAL:
-        from multimodaltraj_2_amd.realdata import real_batch
-        S, H = args.scenes or 128, 128
-        b = real_batch(S, H, seed=1 + rank)
-        Nmax, F = b.pos.shape[2], b.F
+        b = real_scene_batch(args.scenes or 128, 128, rank, world)
+        S, H, Nmax, F = b.S, 128, b.pos.shape[2], b.F
     else:
         cfg = dict(CONFIGS[args.config])
         if args.config in ("eth_ucy_loo_kfold4", "dense_crowd"):
@@ -346,8 +366,9 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": ("real (ETH/UCY batches of the reference's data files, train.py batch walk, "
-                     "stride 0, n_frames = len(batch); N(0,1) weights)" if args.config == REAL else
+            "data": ("real (distinct sample.py scenes of the reference's ETH/UCY files, k-fold-4 "
+                     "training datasets + ETH hotel; stride 0, n_frames = len(batch); N(0,1) "
+                     "weights)" if args.config == REAL else
                      "synthetic (seeded random-walk ETH-shaped scenes; N(0,1) weights)"),
             "mode": "reference (train.py:197-276: forward, recurrence, ADE/FDE; the reference "
                     "has no backward)",

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define G2K_ABI_VERSION 2
+#define G2K_ABI_VERSION 3
 
 enum {
   G2K_OK = 0,
@@ -295,6 +295,55 @@ int64_t g2k_context_conv_workspace_bytes(int32_t Hh, int32_t Ww, int32_t D);
 int g2k_context_conv_f32(const float* img, int32_t Hh, int32_t Ww, int32_t C, const float* filt,
                          int32_t D, float lambda, float* out, float* G, void* workspace,
                          int64_t workspace_bytes, void* stream);
+
+/*
+ * Tensorized data path (a1/a2 of §8(a)).  Host-side
+ * planning (no device memory, callable without a GPU) plus one device gather.
+ *
+ * g2k_traj_create: index over one CSV split — `frame` / `ped` are rows 0 / 1 of
+ *   the split's columns (load_traj.py:133-139: tr_data or val_data), `diff` =
+ *   obs_len.  Keys are every frame value plus the grid seed + k*diff <= max;
+ *   grid keys hold their columns in file order, the others are empty
+ *   (load_traj.py:234-256 frame_preprocess).  Returns an opaque handle, NULL on
+ *   failure.  g2k_traj_destroy frees it.
+ * g2k_traj_next_step: DataLoader.next_step (load_traj.py:153-224) from
+ *   `frame_pointer`: keys[n_keys] = the batch's (non-empty) frame keys in
+ *   x_batch order; the target draws as the drawn frames' columns one frame after
+ *   the other (draw_cols, draw_len[n_draws] columns per draw; each draw appends
+ *   every column pred_len times, quirk Q11); *next_pointer = the advanced
+ *   frame_pointer.  draw_cols / draw_len may be NULL.
+ * g2k_traj_sample_scenes: for each of n frame pointers, next_step then
+ *   ConstructGraph on a fresh graph at framenum 0 with the time slice
+ *   (sample.py:138-164; networkx_graph.py:30-73, 114-129): pos_col [n, 8, nmax]
+ *   = the CSV column holding node j's position list row t (-1: the zero slot —
+ *   a node's first occurrence is not written, rows >= 8 are dropped),
+ *   tgt_col [n, nmax, 12] = the columns of node j's first 12 target entries
+ *   (-1 past the list), n_nodes [n] = nodes in the graph (may exceed nmax: the
+ *   extra nodes are dropped), n_keys [n] = len(batch), next_pointer [n] or NULL.
+ *   Node order is the graph's insertion order.
+ * g2k_scene_gather_f32: expands those plans on the device: xy [cols, 2] (rows
+ *   2:4 of the split, fp32), vis [2, cols] or NULL (rows 4:6; ETH: none, Q14)
+ *   -> pos [S, 8, Nmax, 2] (slot -1: 0), vislet [S, 2, Nmax] = vis[:, vis_off[s]
+ *   + n] (train.py:182 / sample.py:184; vis_off NULL = 0), targets
+ *   [S, F, Nmax, 12, 2] (the same 12 points for every frame: the reference
+ *   feeds one batch's targets to every frame of its loop), ped_mask [S, Nmax]
+ *   (1: n < n_active and all 12 target columns present).  Columns >= n_active
+ *   are zero.
+ */
+void* g2k_traj_create(const double* frame, const double* ped, int64_t cols, int32_t diff);
+void g2k_traj_destroy(void* traj);
+int g2k_traj_next_step(const void* traj, double frame_pointer, int32_t batch_size, int32_t obs_len,
+                       double* keys, int32_t max_keys, int32_t* n_keys, int64_t* draw_cols,
+                       int64_t max_draw_cols, int64_t* draw_len, int32_t* n_draws,
+                       double* next_pointer);
+int g2k_traj_sample_scenes(const void* traj, const double* frame_pointers, int32_t n,
+                           int32_t batch_size, int32_t obs_len, int32_t pred_len, int32_t nmax,
+                           int32_t* pos_col, int32_t* tgt_col, int32_t* n_nodes, int32_t* n_keys,
+                           double* next_pointer);
+int g2k_scene_gather_f32(const float* xy, const float* vis, int64_t cols, const int32_t* pos_col,
+                         const int32_t* tgt_col, const int32_t* vis_off, const int32_t* n_active,
+                         int32_t S, int32_t F, int32_t Nmax, float* pos, float* vislet,
+                         float* targets, uint8_t* ped_mask, void* stream);
 
 #ifdef __cplusplus
 }

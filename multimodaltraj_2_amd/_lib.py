@@ -69,9 +69,17 @@ SYMBOLS = {
     "g2k_context_conv_workspace_bytes": (c_i64, [c_i32, c_i32, c_i32]),
     "g2k_context_conv_f32": (c_int, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp,
                                      c_vp, c_i64, c_vp]),
+    "g2k_traj_create": (c_vp, [c_vp, c_vp, c_i64, c_i32]),
+    "g2k_traj_destroy": (None, [c_vp]),
+    "g2k_traj_next_step": (c_int, [c_vp, ctypes.c_double, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp,
+                                   c_i64, c_vp, c_vp, c_vp]),
+    "g2k_traj_sample_scenes": (c_int, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp,
+                                       c_vp, c_vp, c_vp]),
+    "g2k_scene_gather_f32": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
+                                     c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class G2KLibraryError(RuntimeError):

@@ -1,6 +1,7 @@
 """Flags of the reference (argParser.py:3-73), same names and defaults, plus
-the build's own: --data_root (Q8), --device, --slice, --chain_hidden,
---log_dir, --seed."""
+the build's own: --data_root (Q8), --device, --mode,
+--world_size, --n_max, --train_batch, --train_scenes, --valid_from_seed,
+--log_dir, --save_dir, --seed."""
 import argparse
 
 
@@ -31,10 +32,18 @@ class ArgsParser:
     parser.add_argument('--data_root', type=str, default='data',
                         help='directory holding eth/ and ucy/ (replaces hard-coded paths, Q8)')
     parser.add_argument('--device', type=str, default='cuda')
-    parser.add_argument('--slice', choices=('train', 'sample'), default='train',
-                        help="batch_v slice: train.py node slice (Q10) or sample.py time slice")
-    parser.add_argument('--chain_hidden', type=int, default=1,
-                        help='carry hidden_state from batch to batch like train.py')
+    parser.add_argument('--mode', choices=('reference', 'train'), default='reference',
+                        help="reference: train.py's legs (no loss, as the reference); train: "
+                             "RMSProp on the L2 loss over the fold's real scenes, data parallel")
+    parser.add_argument('--world_size', type=int, default=0,
+                        help='--mode train: expected ranks (torchrun WORLD_SIZE; 0: any)')
+    parser.add_argument('--n_max', type=int, default=0,
+                        help='--mode train: pedestrian padding Nmax (0: the largest scene, '
+                             'rounded up to 16; larger scenes are left out)')
+    parser.add_argument('--train_batch', type=int, default=256,
+                        help='--mode train: scenes per global step (a multiple of the ranks)')
+    parser.add_argument('--train_scenes', type=int, default=0,
+                        help='--mode train: distinct scenes used (0: all of the fold)')
     parser.add_argument('--valid_from_seed', type=int, default=0,
                         help="validation leg from the file's first frame (the reference starts "
                              "at frame 0, which the ETH/UCY frame keys never hit)")

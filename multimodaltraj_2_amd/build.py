@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SRC = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+CXX_SRC = sorted(glob.glob(os.path.join(CSRC, "*.cpp")))   # host-only C++ (g++)
 HDR = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "g2k_hip.h")]
 OUT = os.path.join(HERE, "libg2k_hip.so")
 OBJ = os.path.join(HERE, "build")
@@ -34,12 +35,19 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in SRC + HDR + [os.path.abspath(__file__)])
+    return any(os.path.getmtime(p) > t for p in SRC + CXX_SRC + HDR + [os.path.abspath(__file__)])
+
+
+CXX = os.environ.get("CXX", "g++")
+CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-I" + os.path.join(ROOT, "include")]
 
 
 def _compile(src, verbose):
-    obj = os.path.join(OBJ, os.path.basename(src)[:-4] + ".o")
-    cmd = [HIPCC, *flags_for(src), "-c", "-o", obj, src]
+    obj = os.path.join(OBJ, os.path.splitext(os.path.basename(src))[0] + ".o")
+    if src.endswith(".cpp"):
+        cmd = [CXX, *CXX_FLAGS, "-c", "-o", obj, src]
+    else:
+        cmd = [HIPCC, *flags_for(src), "-c", "-o", obj, src]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
@@ -50,7 +58,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if force or needs_build():
         os.makedirs(OBJ, exist_ok=True)
         with ThreadPoolExecutor(max_workers=min(8, len(SRC))) as ex:
-            objs = list(ex.map(lambda s: _compile(s, verbose), SRC))
+            objs = list(ex.map(lambda s: _compile(s, verbose), SRC + CXX_SRC))
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

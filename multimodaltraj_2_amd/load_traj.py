@@ -25,6 +25,67 @@ import os
 
 import numpy as np
 
+class TrajIndex:
+    """Native index over one CSV split (g2k_traj_create; csrc/g2k_walk.cpp):
+    the frame dict's keys and rows, and the reference's batch walk over them.
+    Host code only: usable without a GPU."""
+
+    def __init__(self, frames, peds, diff):
+        from . import _lib
+        self._lib = _lib.load()
+        self.frames = np.ascontiguousarray(frames, dtype=np.float64)
+        peds = np.ascontiguousarray(peds, dtype=np.float64)
+        self.cols = int(self.frames.shape[0])
+        self._h = self._lib.g2k_traj_create(self.frames.ctypes.data, peds.ctypes.data, self.cols,
+                                            int(diff))
+        if not self._h:
+            _lib.check("g2k_traj_create", -1)
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.g2k_traj_destroy(h)
+
+    def next_step(self, frame_pointer, batch_size, obs_len):
+        """-> (batch keys [k] float64, drawn columns, columns per draw, new
+        frame pointer); load_traj.py:153-224."""
+        import ctypes
+        from . import _lib
+        cap = max(4 * batch_size, 64)
+        keys = np.empty(cap, np.float64)
+        nk, nd, nxt = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_double()
+        dlen = np.empty(cap * batch_size, np.int64)
+        rc = self._lib.g2k_traj_next_step(self._h, float(frame_pointer), batch_size, obs_len,
+                                          keys.ctypes.data, cap, ctypes.byref(nk), None, 0,
+                                          dlen.ctypes.data, ctypes.byref(nd), ctypes.byref(nxt))
+        _lib.check("g2k_traj_next_step", rc)
+        dlen = dlen[:nd.value]
+        cols = np.empty(max(int(dlen.sum()), 1), np.int64)
+        rc = self._lib.g2k_traj_next_step(self._h, float(frame_pointer), batch_size, obs_len,
+                                          keys.ctypes.data, cap, ctypes.byref(nk), cols.ctypes.data,
+                                          cols.size, dlen.ctypes.data, ctypes.byref(nd),
+                                          ctypes.byref(nxt))
+        _lib.check("g2k_traj_next_step", rc)
+        return keys[:nk.value].copy(), cols, dlen, nxt.value
+
+    def sample_scenes(self, frame_pointers, nmax, batch_size=16, obs_len=8, pred_len=12):
+        """sample.py:138-164 scenes for many frame pointers at once ->
+        dict(pos_col [n, 8, nmax], tgt_col [n, nmax, 12], n_nodes [n],
+        n_keys [n], next_pointer [n]) (g2k_traj_sample_scenes)."""
+        from . import _lib
+        fps = np.ascontiguousarray(frame_pointers, dtype=np.float64).reshape(-1)
+        n = int(fps.size)
+        out = dict(pos_col=np.empty((n, 8, nmax), np.int32), tgt_col=np.empty((n, nmax, 12), np.int32),
+                   n_nodes=np.empty(n, np.int32), n_keys=np.empty(n, np.int32),
+                   next_pointer=np.empty(n, np.float64))
+        rc = self._lib.g2k_traj_sample_scenes(
+            self._h, fps.ctypes.data, n, batch_size, obs_len, pred_len, nmax,
+            out["pos_col"].ctypes.data, out["tgt_col"].ctypes.data, out["n_nodes"].ctypes.data,
+            out["n_keys"].ctypes.data, out["next_pointer"].ctypes.data)
+        _lib.check("g2k_traj_sample_scenes", rc)
+        return out
+
+
 DATA_DIRS = ["eth/hotel/", "eth/univ/", "ucy/zara/zara01/", "ucy/zara/zara02/", "ucy/univ/",
              "town_center.csv", "annotation_tc.txt"]     # load_traj.py:25-33
 
@@ -53,7 +114,7 @@ class DataLoader:
             if not files:
                 raise FileNotFoundError(f"no CSV under {self.current_dir}")
             self.load_dataset(files[int(self.dataset_pointer)], val=infer)
-        self.trajectories = self.frame_preprocess()
+        self._traj = None          # the frame dict, built on first use
         self.num_batches = int((len(self.frameList) / self.seq_length) / self.batch_size)
 
     # load_traj.py:114-150
@@ -74,6 +135,16 @@ class DataLoader:
         self.vislet = src[4:6, :] if src.shape[0] >= 6 else np.zeros((2, src.shape[1]))
         self.seed = self.frameList[0]
         self.frame_pointer = self.seed
+        self._fmax = self.frameList.max()          # max(self.frameList), load_traj.py:163
+        self.index = TrajIndex(self.frameList, src[1, :], self.diff)
+
+    @property
+    def trajectories(self):
+        """The frame dict {frame: [{ped: [x, y]}, ...]} (load_traj.py:234-256),
+        built on first use (the native index plans the walk without it)."""
+        if self._traj is None:
+            self._traj = self.frame_preprocess()
+        return self._traj
 
     def frame_preprocess(self, data_file=None, seed=0):
         """load_traj.py:234-256: {frame: [{ped: [x, y]}, ...]}; every frame of
@@ -84,8 +155,8 @@ class DataLoader:
         rows = {}
         for (ind, ped, px, py) in np.transpose(self.pedsPerFrameList):
             rows.setdefault(ind, []).append({ped: [px, py]})
-        fp = self.frame_pointer
-        fmax = self._fmax = max(self.frameList)
+        fp = self.seed
+        fmax = self._fmax
         while fp <= fmax:
             frame_data[fp] = rows.get(fp, [])
             fp += self.diff
@@ -94,57 +165,37 @@ class DataLoader:
     def next_step(self, targets=None):
         """Batch of frame dicts + target lists; contract of load_traj.py:153-224.
 
-        Up to batch_size + 1 passes; each pass appends the frames
-        frame_pointer, +diff, ... (batch_size keys, stopping at the first
-        missing key) to a growing window, then walks the window in insertion
-        order with a single cursor that the reference advances once per
-        visited key and once more per target draw (its ``iter_traj``).  Every
-        obs_len-th visit draws the frame under the cursor and appends each of
-        its pedestrians' positions pred_len times to ``targets`` (quirk Q11).
-        A pass stops the walk when the cursor runs out; the last key touched
-        feeds the end-of-data test of the next pass."""
+        The walk itself (which keys the batch holds, which frames are drawn
+        as targets, the new frame pointer) is planned natively
+        (``TrajIndex.next_step``, csrc/g2k_walk.cpp); this builds the
+        reference's dicts from the plan: the batch's frames in x_batch order,
+        and for every draw each of the drawn frame's pedestrians' positions
+        appended pred_len times (quirk Q11; the position objects are the frame
+        dict's own, as the reference appends them)."""
         tgt = {} if targets is None else targets
-        batch, window = {}, {}
-        visits = 1                                   # `pc`, kept across passes
-        fmax = self._fmax
-        last = self.frame_pointer
-        span = self.batch_size * self.obs_len
-        for _ in range(self.batch_size + 1):
-            if fmax - (last + 1) <= 0:
-                break
-            # the log-scale test of :175-177 always holds once the gap is > 0
-            for key in range(int(self.frame_pointer), int(self.frame_pointer + span), self.diff):
-                last = key
-                if key not in self.trajectories:
-                    break
-                window[key] = self.trajectories[key]
-            order = list(window)
-            cursor = 0
-            for key in order:
-                last = key
-                frame = self.trajectories[key]
-                if len(frame):
-                    batch[key] = frame
-                    if visits % self.obs_len == 0:
-                        if cursor >= len(order):
-                            break
-                        drawn = self.trajectories[order[cursor]]
-                        cursor += 1
-                        for _rep in range(int(self.pred_len)):
-                            for entry in drawn:
-                                (pid, xy), = entry.items()
-                                pid = int(pid)
-                                if not tgt:
-                                    tgt = {pid: [xy]}      # rebinding, as the reference
-                                elif pid in tgt:
-                                    tgt[pid].append(xy)
-                                else:
-                                    tgt[pid] = [xy]
-                visits += 1
-                if cursor >= len(order):
-                    break
-                cursor += 1
-            self.frame_pointer += self.diff
+        keys, draw_cols, draw_len, fp = self.index.next_step(self.frame_pointer, self.batch_size,
+                                                             self.obs_len)
+        batch = {int(k): self.trajectories[k] for k in keys}
+        reps = int(self.pred_len)
+        at = 0
+        for n in draw_len:
+            if n == 0:
+                continue
+            entries = self.trajectories[self.frameList[draw_cols[at]]]
+            at += n
+            ids = [int(next(iter(e))) for e in entries]
+            if len(set(ids)) == len(ids):
+                for pid, e in zip(ids, entries):
+                    xy = next(iter(e.values()))
+                    if pid in tgt:
+                        tgt[pid].extend([xy] * reps)
+                    else:
+                        tgt[pid] = [xy] * reps
+            else:                       # a pedestrian twice in one frame: the exact order
+                for _ in range(reps):
+                    for pid, e in zip(ids, entries):
+                        tgt.setdefault(pid, []).append(next(iter(e.values())))
+        self.frame_pointer = fp
         return batch, tgt, self.frame_pointer
 
     def tick_frame_pointer(self, valid=False, incr=8):

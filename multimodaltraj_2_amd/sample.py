@@ -56,16 +56,20 @@ def restore_weights(save_dir, device):
     return checkpoint.load_params(prefix, device=device)
 
 
-def model_weights(restored, n, D, T, seed, device):
+def model_weights(restored, n, D, T, seed, device, log=print):
     """g2k_lstm_mcr weights for a batch of n pedestrians: the restored ones,
-    weight_o's missing columns (and everything without a checkpoint) N(0, 1)."""
+    weight_o's missing columns (and everything without a checkpoint) N(0, 1).
+    A checkpoint of another hidden_len (train.py writes D = 16, sample.py runs
+    D = num_freq_blocks = 10) cannot be used: N(0, 1) weights, with a warning."""
     rng = np.random.default_rng(seed)
     draw = lambda shape: torch.from_numpy(rng.standard_normal(shape).astype(np.float32)).to(device)
     w = dict(weight_v=draw((T, D + 2)), bias_v=draw((D,)), weight_o=draw((T, n)),
              weight_c=draw((2 * fs.PRED_LEN, T)), weight_r=draw((T, 2)))
+    if restored is not None and tuple(restored.Wv.shape) != (T, D + 2):
+        log(f"checkpoint weight_v {tuple(restored.Wv.shape)} is not [{T}, {D + 2}] (D = "
+            f"num_freq_blocks = {D}): its weights are not used, N(0, 1) instead")
+        restored = None
     if restored is not None:
-        if tuple(restored.Wv.shape) != (T, D + 2):
-            raise ValueError(f"checkpoint weight_v {tuple(restored.Wv.shape)} does not match D = {D}")
         k = min(n, int(restored.Wo.shape[1]))
         wo = w["weight_o"].clone()
         wo[:, :k] = restored.Wo[:, :k]

@@ -67,6 +67,39 @@ def build_scene(batch, target_traj, graph_t, loader, frame, *, mode="train", obs
     return RealScene(window, vis, targets, mask, len(batch), keys)
 
 
+def scene_from_record(rec, loader, *, pairing="row", pred_len=12):
+    """A walks.WalkBatch (n >= 0) -> RealScene: its window (the node slice of
+    train.py:78 / the time slice of sample.py:154), the vislet columns
+    [vis_off, vis_off + n) of the split (train.py:182, 527; zero past the
+    split's end, where the reference's matmul would fail), and the targets of
+    ``pairing`` (see build_scene); n_frames = len(batch)."""
+    n = max(int(rec.n), 0)
+    window = rec.window if rec.window is not None else np.zeros((8, 0, 2))
+    vis = np.zeros((2, n))
+    src = loader.vislet[:, rec.vis_off:rec.vis_off + n]
+    vis[:, :src.shape[1]] = src
+    tt = rec.target_traj
+    keys = list(tt.keys())
+    targets = np.zeros((n, pred_len, 2))
+    mask = np.zeros(n, bool)
+    if pairing == "row":
+        rows = [(i, keys[i]) for i in range(min(n, len(keys)))]
+    elif pairing == "train_log":
+        rows = [(i, itr) for i, itr in zip(range(1, n), keys) if i in tt]
+    elif pairing == "node":                       # sample.py: each node's own targets
+        rows = [(i, None) for i in range(n)]
+    else:
+        raise ValueError(f"pairing {pairing!r}")
+    for i, k in rows:
+        seq = rec.extra["node_targets"][i] if k is None else tt[k]
+        t = np.asarray(seq, dtype=np.float64).reshape(-1, 2)
+        if len(t) >= pred_len and (pairing != "train_log" or len(tt[i]) >= pred_len):
+            targets[i] = t[:pred_len]
+            mask[i] = True
+    return RealScene(np.asarray(window, np.float64).reshape(8, n, 2), vis, targets, mask,
+                     rec.n_frames, keys)
+
+
 def train_log_vectors(pred_path_band, target_traj, pred_len=12):
     """train.py:254-276 for one frame's pred_path_band [2, L, N]: the raw
     difference vectors the training leg logs (train.py:348-351), row i >= 1

@@ -40,3 +40,25 @@ def gpu():
     from multimodaltraj_2_amd import _lib
     _lib.load()   # fails loudly if the HIP library is missing
     return torch.device("cuda:0")
+
+
+FIXTURE_DIRS = {"eth_hotel": "eth/hotel/", "zara01": "ucy/zara/zara01/",
+                "zara02": "ucy/zara/zara02/", "ucy_univ": "ucy/univ/"}
+
+
+def write_data_root(root, names=tuple(FIXTURE_DIRS)):
+    """A data root laid out as the reference's data/ (load_traj.py:25-33)
+    holding the committed raw CSV arrays (tests/golden/data_*.npz), written
+    with 17 significant digits so np.genfromtxt reads back the same float64."""
+    import numpy as np
+    for n in names:
+        d = os.path.join(str(root), FIXTURE_DIRS[n])
+        os.makedirs(d, exist_ok=True)
+        raw = np.load(os.path.join(ROOT, "tests", "golden", f"data_{n}.npz"))["raw_data"]
+        np.savetxt(os.path.join(d, "data.csv"), raw, delimiter=",", fmt="%.17g")
+    return str(root)
+
+
+@pytest.fixture(scope="session")
+def data_root(tmp_path_factory):
+    return write_data_root(tmp_path_factory.mktemp("data"))

@@ -1,69 +1,83 @@
-"""GPU: config 3's workload on real data — many ETH/UCY batches (four of the
-reference's data files, tests/golden/data_*.npz) packed into ONE [S, ...]
-launch (multimodaltraj_2_amd/realdata.py: stride 0, per-scene n_frames and
-ped_mask, chain cut) through g2k_step_fused_f32 and g2k_step_grad_f32 vs the
-float64 oracle scene by scene.  Tolerances as tests/test_step_gpu.py /
-tests/test_train_gpu.py."""
+"""GPU: config 3's workload on real data — 128 DISTINCT ETH/UCY scenes (the
+reference's data files, tests/golden/data_*.npz; multimodaltraj_2_amd/realdata.py:
+sample.py's scene per frame pointer, planned natively and expanded by
+g2k_scene_gather_f32) in ONE [S, ...] launch of g2k_step_fused_f32 and
+g2k_step_grad_f32, EVERY scene checked against the float64 oracle.
+Tolerances as tests/test_step_gpu.py / tests/test_train_gpu.py."""
 import numpy as np
 import pytest
 import torch
 
 from multimodaltraj_2_amd import frame_step as fs
+from multimodaltraj_2_amd import realdata as rd
 from multimodaltraj_2_amd import train_step as ts
-from multimodaltraj_2_amd.realdata import real_batch
 from oracle import g2k_ref as ref
 from tests.conftest import close, close_h
+from tests.test_realdata import RAW
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
+H = 128
 
 
 @pytest.fixture(scope="module")
-def batch():
-    return real_batch(64, 128, seed=3)
+def plan():
+    return rd.plan_scenes(128, RAW)
 
 
-def test_real_batch_packs_many_datasets(batch):
-    assert batch.S == 64 and batch.stride == 0
-    assert len(set(batch.n_frames.tolist())) > 1          # ragged frame counts across scenes
-    assert batch.ped_mask.any() and not batch.ped_mask.all()
-
-
-def test_real_launch_matches_oracle(gpu, batch):
-    b = batch
-    Nmax = b.pos.shape[2]
-    params = fs.init_params(Nmax, seed=0, device=gpu)
-    t = b.to_device(gpu)
-    plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
-                       n_frames=t["n_frames"], ped_mask=t["ped_mask"], stride=0)
-    out = plan.run()
+@pytest.fixture(scope="module")
+def dev_batch(gpu, plan):
+    t = plan.to_device(gpu)
     torch.cuda.synchronize()
-    w = params.numpy()
-    for s in range(0, b.S, 4):
-        n, nf = int(b.n_active[s]), int(b.n_frames[s])
-        pr, h, m, _ = ref.scene_step(b.pos[s], b.vislet[s], b.G[s], w, b.targets[s], n, b.h0[s],
-                                     n_frames=nf, stride=0, ped_mask=b.ped_mask[s].astype(bool))
-        got = out.pred[s, :nf, :, :n].cpu().numpy().reshape(nf, 2, 12, n)
-        assert close(got, pr) <= TOL
-        assert close_h(out.h[s].cpu().numpy(), h)
-        assert close(out.metrics[s, :6].cpu().numpy(), m[:6]) <= TOL
+    rng = np.random.default_rng(3)
+    t["G"] = torch.from_numpy(rng.standard_normal((plan.S, 16, 8)).astype(np.float32)).to(gpu)
+    t["h0"] = torch.zeros((plan.S, 16, H), device=gpu)
+    return t
 
 
-def test_real_launch_gradient_matches_oracle(gpu, batch):
-    b = batch
-    S = 16
-    Nmax = b.pos.shape[2]
+def test_device_gather_equals_host_expansion(plan, dev_batch):
+    h = plan.host()
+    for k in ("pos", "vislet", "targets", "ped_mask", "n_active", "n_frames"):
+        np.testing.assert_array_equal(dev_batch[k].cpu().numpy(), h[k], err_msg=k)
+
+
+def test_every_real_scene_matches_oracle(gpu, plan, dev_batch):
+    t = dev_batch
+    Nmax = plan.Nmax
     params = fs.init_params(Nmax, seed=0, device=gpu)
-    t = {k: (v[:S] if isinstance(v, torch.Tensor) else v) for k, v in b.to_device(gpu).items()}
+    out = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
+                      n_frames=t["n_frames"], ped_mask=t["ped_mask"], stride=0).run()
+    torch.cuda.synchronize()
+    h = plan.host()
+    G = t["G"].cpu().numpy()
+    w = params.numpy()
+    pred, hh, met = out.pred.cpu().numpy(), out.h.cpu().numpy(), out.metrics.cpu().numpy()
+    for s in range(plan.S):
+        n, nf = int(plan.n_active[s]), int(plan.n_frames[s])
+        pr, h_ref, m, _ = ref.scene_step(h["pos"][s], h["vislet"][s], G[s], w, h["targets"][s], n,
+                                         np.zeros((16, H), np.float32), n_frames=nf, stride=0,
+                                         ped_mask=h["ped_mask"][s].astype(bool))
+        assert close(pred[s, :nf, :, :n].reshape(nf, 2, 12, n), pr) <= TOL, s
+        assert close_h(hh[s], h_ref), s
+        assert close(met[s, :6], m[:6]) <= TOL, s
+
+
+def test_real_launch_gradient_matches_oracle(gpu, plan, dev_batch):
+    S = 32
+    Nmax = plan.Nmax
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    t = {k: (v[:S] if isinstance(v, torch.Tensor) else v) for k, v in dev_batch.items()}
     gp = ts.GradPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
                      n_frames=t["n_frames"], ped_mask=t["ped_mask"], stride=0)
     g = gp.run().double().cpu().numpy()
+    h = plan.host()
+    G = dev_batch["G"].cpu().numpy()
     w = params.numpy()
     loss, cnt, R = 0.0, 0, None
     for s in range(S):
-        l_, c_, r_ = ref.scene_loss_grad(b.pos[s], b.vislet[s], b.G[s], w, b.targets[s],
-                                         int(b.n_active[s]), n_frames=int(b.n_frames[s]), stride=0,
-                                         ped_mask=b.ped_mask[s].astype(bool))
+        l_, c_, r_ = ref.scene_loss_grad(h["pos"][s], h["vislet"][s], G[s], w, h["targets"][s],
+                                         int(plan.n_active[s]), n_frames=int(plan.n_frames[s]),
+                                         stride=0, ped_mask=h["ped_mask"][s].astype(bool))
         loss += l_
         cnt += c_
         R = r_ if R is None else {k: R[k] + r_[k] for k in R}
@@ -79,3 +93,18 @@ def test_real_launch_gradient_matches_oracle(gpu, batch):
             assert np.abs(got - r).max() <= TOL * max(np.abs(r).max(), 1e-30), k
     assert off == P
     assert abs(g[P] - loss) <= TOL * loss and g[P + 1] == cnt
+
+
+def test_1024_scene_batch_built_fast(gpu):
+    """A 1024-scene real batch, planned natively and gathered on the device,
+    in well under a second (the walk of round 2 took 83 s)."""
+    import time
+    srcs = [rd.SceneSource(n, RAW[n]) for n in RAW]
+    t0 = time.perf_counter()
+    p = rd.plan_scenes(1024, RAW, sources=srcs)
+    t = p.to_device(gpu)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert t["targets"].shape[0] == 1024
+    print(f"1024 real scenes planned + gathered in {dt * 1e3:.1f} ms")
+    assert dt < 0.5

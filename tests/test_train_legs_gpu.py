@@ -1,127 +1,127 @@
-"""GPU: train.py's two legs on the committed data fixtures vs the float64
-oracle.  Training leg: the training log's pairing (row i against key i - 1,
-train.py:257-276) and its raw difference vectors (train.py:254-276, 346-351)
-from the HIP step's predictions == oracle.train_log_errors on the oracle's
-predictions; the CSV files the leg writes.  Validation leg (train.py:371-695):
-per-batch cross-validation ADE / FDE == oracle.batch_metrics of the oracle
-step (including the leave-dataset-5 divisor).  Tolerance 1e-4 * max(1, |ref|)."""
+"""GPU: train.py's two legs through the entry point (multimodaltraj_2_amd/train.py)
+on the reference's data files (tests/golden/data_*.npz written as a data root)
+vs the float64 oracle run batch by batch over the same walk.
+
+Training leg: every batch of every epoch of the fold's first dataset (the
+reference's e / frame / counters are set once per left-out dataset,
+train.py:29-36), in one launch per epoch, the hidden state chained batch after
+batch: the raw-vector logs (train.py:254-276, 346-351) == oracle.train_log_errors
+on the oracle's predictions, the chained h == the oracle's sequential chain, the
+counts file == the reference replay's counters (tests/golden/walk_*.npz).
+Validation leg: fresh graph, frame = 1 (train.py:374, 392); per-batch ADE / FDE
+== oracle.batch_metrics; train() end to end validates the same way.
+Tolerance 1e-4 * max(1, |ref|); h: close_h."""
 import os
+from types import SimpleNamespace
 
 import numpy as np
 import pytest
 import torch
 
-from multimodaltraj_2_amd import networkx_graph as nxg
+from multimodaltraj_2_amd import frame_step as fs
 from multimodaltraj_2_amd import train as tr
+from multimodaltraj_2_amd import walks
 from multimodaltraj_2_amd.argParser import ArgsParser
 from multimodaltraj_2_amd.load_traj import DataLoader
-from multimodaltraj_2_amd.scenes import build_scene, pack
+from multimodaltraj_2_amd.scenes import pack, scene_from_record
 from oracle import g2k_ref as ref
-from tests.conftest import close
+from tests.conftest import close, close_h
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+FIRST = {3: ("zara01", 2), 2: ("zara02", 3)}       # leaveDataset -> the fold's first dataset
 
 
-def _args(tmp_path, leave=2):
+def _args(tmp_path, data_root, leave, epochs=3):
     a = ArgsParser().parser.parse_args([])
-    a.batch_size, a.seq_length, a.pred_len, a.obs_len = 16, 12, 12, 8
-    a.num_epochs, a.log_dir, a.save_dir, a.leaveDataset = 1, str(tmp_path), "", leave
+    a.num_epochs, a.log_dir, a.save_dir, a.leaveDataset = epochs, str(tmp_path), "", leave
+    a.data_root = data_root
     return a
 
 
-def _loader(args, name):
-    return DataLoader(args, raw_data=np.load(os.path.join(GOLDEN, f"data_{name}.npz"))["raw_data"])
-
-
-def _oracle_step(args, sc, h0):
-    pk = pack([sc], args.rnn_size)
-    w = tr.fs.init_params(pk["Nmax"], seed=args.seed).numpy()
-    G = tr._g(args.seed, 16, "cpu")[0].numpy()
+def _oracle_record(args, loader, rec, pairing, h0):
+    sc = scene_from_record(rec, loader, pairing=pairing)
+    pk = pack([sc], args.rnn_size, nmax=tr.NODE_SLICE_NMAX)
+    w = fs.init_params(tr.NODE_SLICE_NMAX, seed=args.seed).numpy()
+    G = tr.context_G(args.seed)[0]
     n = int(pk["n_active"][0])
     return ref.scene_step(pk["pos"][0], pk["vislet"][0], G, w, pk["targets"][0], n, h0,
                           n_frames=int(pk["n_frames"][0]), stride=0, lam=args.lambda_param,
-                          ped_mask=pk["ped_mask"][0].astype(bool)), n
+                          ped_mask=pk["ped_mask"][0].astype(bool))
 
 
-@pytest.mark.parametrize("name", ["zara01", "ucy_univ"])
-def test_training_leg_log_vectors(gpu, tmp_path, name):
-    args = _args(tmp_path)
-    loader = _loader(args, name)
-    loader.reset_data_pointer()
-    graph = nxg.online_graph(args)
-    cache, tlog = {}, tr.TrainLog()
-    h = torch.zeros((1, 16, args.rnn_size), device=gpu)
+@pytest.mark.parametrize("leave", [3, 2])
+def test_training_leg_every_batch(gpu, tmp_path, data_root, leave):
+    name, d = FIRST[leave]
+    args = _args(tmp_path, data_root, leave)
+    params = tr.leg_params(args, gpu)
+    summary, h, counters = tr.training_leg(args, gpu, params, log=lambda s: None)
+    # the oracle over the same walk, batch after batch, h chained
+    loader = DataLoader(args, datasets=[0, 1, 2, 3, 4, 5], start=d, sel=0, data_root=data_root)
     h_ref = np.zeros((16, args.rnn_size))
-    frame, checked = 1, 0
-    for b in range(min(loader.num_batches, 12)):
-        batch, tgt, _ = loader.next_step()
-        if len(batch) == 0:
-            break
-        g = graph.ConstructGraph(current_batch=batch, framenum=int(frame), future_traj=tgt)
-        sc = build_scene(batch, tgt, g, loader, frame, pairing="train_log")
-        for k in batch:
-            frame = k
-        if sc.window.shape[1] < 2:
+    euc, fde, ran = [], [], 0
+    for rec in walks.train_walk(loader, args, args.num_epochs):
+        if isinstance(rec, str) or rec.n < 0:
             continue
-        out, _ = tr._step(args, sc, cache, h, gpu)
-        h = out.h
-        n0 = len(tlog.euc)
-        tlog.add(out.pred[0], sc.n_frames, sc.window.shape[1], tgt)
-        (pr, h_ref, m, _), n = _oracle_step(args, sc, h_ref)
-        euc, fde = [], []
-        for f in range(pr.shape[0]):
-            e, d = ref.train_log_errors(pr[f], tgt)
-            euc += e
-            fde += d
-        assert len(tlog.euc) - n0 == len(euc) and len(euc) > 0
-        for got, want in zip(tlog.euc[n0:], euc):
-            assert close(got, want) <= TOL
-        for got, want in zip(tlog.fde[n0:], fde):
-            assert close(got, want) <= TOL
-        checked += 1
-    assert checked >= 1
-    tlog.write(str(tmp_path), 3)
-    fde_csv = np.loadtxt(tmp_path / "g2k_MPC_fde_log_kfold_3.csv", delimiter=",")
-    euc_csv = np.loadtxt(tmp_path / "g2k_MPC_error_log_kfold_3.csv", delimiter=",")
-    assert fde_csv.shape == (len(tlog.fde), 2)
-    assert euc_csv.size == sum(e.size for e in tlog.euc)
+        pr, h_ref, m, _ = _oracle_record(args, loader, rec, "train_log", h_ref)
+        for f in range(rec.n_frames):
+            e_, d_ = ref.train_log_errors(pr[f], rec.target_traj)
+            euc += e_
+            fde += d_
+        ran += 1
+    assert ran == len(summary[d]) and ran > 3
+    assert close_h(h[0].cpu().numpy(), h_ref)
+    got_f = np.loadtxt(tmp_path / f"g2k_MPC_fde_log_kfold_{d}.csv", delimiter=",").reshape(-1, 2)
+    got_e = np.loadtxt(tmp_path / f"g2k_MPC_error_log_kfold_{d}.csv", delimiter=",")
+    assert len(fde) > 0 and got_f.shape == (len(fde), 2)
+    assert close(got_f, np.array(fde)) <= TOL
+    assert close(got_e, np.concatenate([np.ravel(x) for x in euc])) <= TOL
+    # the counts file: the reference replay's counters after the last batch
+    z = np.load(os.path.join(GOLDEN, f"walk_{name}.npz"))
+    ok = z["tw_n"] >= 0
+    want_t, want_e = int(z["tw_num_targets"][ok][-1]), int(z["tw_num_end_targets"][ok][-1])
+    for dd in sorted({2, 3, 4} - {leave}):              # every dataset of the fold writes one
+        txt = open(tmp_path / f"g2k_lstm_counts_{dd}.txt").read()
+        assert txt == f"Dataset {dd}= ADE steps {want_t}\nFDE steps = {want_e}"
 
 
-@pytest.mark.parametrize("name,leave", [("zara01", 2), ("ucy_univ", 5)])
-def test_validation_leg_matches_oracle(gpu, tmp_path, name, leave):
-    args = _args(tmp_path, leave)
-    cache = {}
+@pytest.mark.parametrize("name,d,leave", [("zara01", 2, 2), ("ucy_univ", 4, 5)])
+def test_validation_leg_matches_oracle(gpu, tmp_path, data_root, name, d, leave):
+    args = _args(tmp_path, data_root, leave)
+    params = tr.leg_params(args, gpu)
     logs = []
+    mk = lambda: DataLoader(args, datasets=[0, 1, 2, 3, 4, 5], start=d, sel=0,  # noqa: E731
+                            data_root=data_root)
     # the reference's frame pointer 0 finds no key of these files: no batch
-    assert tr.validate(args, 1, None, {}, gpu, log=logs.append, loader=_loader(args, name)) == ([], [])
-    ade, fde = tr.validate(args, 1, None, cache, gpu, log=logs.append, loader=_loader(args, name),
-                           start_pointer=None)
-    # the oracle over the same batches (same pointers, pairing and h chain)
-    loader = _loader(args, name)
-    loader.reset_data_pointer(valid=True, frame_pointer=loader.seed)
-    loader.valid_frame_pointer = int((loader.len - int(loader.max * .7)) / loader.val_max)
-    graph = nxg.online_graph(args)
+    assert tr.validate(args, gpu, params, log=logs.append, loader=mk()) == ([], [])
+    ade, fde = tr.validate(args, gpu, params, log=logs.append, loader=mk(), start_pointer=None)
+    loader = mk()
     h_ref = np.zeros((16, args.rnn_size))
     want_a, want_f = [], []
-    frame = 1
-    for vb in range(int(loader.val_max / loader.batch_size)):   # noqa: B007
-        batch, tgt, fp = loader.next_step()
-        if len(batch) == 0:
+    for rec in walks.valid_walk(loader, args, start_pointer=loader.seed):
+        if rec.n < 0:
             break
-        g = graph.ConstructGraph(current_batch=batch, framenum=fp, future_traj=tgt)
-        sc = build_scene(batch, tgt, g, loader, frame, vislet_offset=loader.valid_frame_pointer)
-        if sc.window.shape[1] < 1:
-            break
-        (pr, h_ref, m, _), n = _oracle_step(args, sc, h_ref)
-        a, f = ref.batch_metrics(m, leave_dataset=leave, num_nodes=n)
-        if np.isfinite(a):
-            want_a.append(a)
-            want_f.append(f)
-        for k in batch:
-            frame = k
-        loader.frame_pointer = frame
+        pr, h_ref, m, _ = _oracle_record(args, loader, rec, "row", h_ref)
+        if rec.n > 0:
+            a, f = ref.batch_metrics(m, leave_dataset=leave, num_nodes=rec.n)
+            if np.isfinite(a):
+                want_a.append(a)
+                want_f.append(f)
     assert len(ade) == len(want_a) and len(ade) > 0
     assert close(ade, want_a) <= TOL and close(fde, want_f) <= TOL
     assert any("Cross-Validation total mean error (ADE)" in s for s in logs)
+
+
+def test_train_entry_point_validates_on_a_fresh_graph(gpu, tmp_path, data_root):
+    """train() runs the training leg, then the validation leg from frame 1 on
+    a fresh graph (train.py:374, 392) — the same numbers as validate() alone."""
+    args = _args(tmp_path, data_root, 2, epochs=1)
+    args.valid_from_seed, args.device = 1, "cuda:0"
+    logs = []
+    tr.train(args, log=logs.append)
+    alone = []
+    tr.validate(args, gpu, tr.leg_params(args, gpu), log=alone.append, start_pointer=None)
+    got = [s for s in logs if s.startswith("Cross-Validation")]
+    assert got == [s for s in alone if s.startswith("Cross-Validation")] and len(got) == 2
+    assert os.path.exists(tmp_path / "g2k_lstm_counts_3.txt")

@@ -36,6 +36,7 @@ import numpy as np
 
 REF = "/root/reference"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 OUT = os.path.join(ROOT, "tests", "golden")
 
 DATASETS = {  # name -> (dir relative to data/, csv selection index 0)
@@ -56,6 +57,89 @@ def frame_dict_from_csv(dl):
         frame_data[fp] = [{ped: [px, py]} for (ind, ped, px, py) in ppfl if ind == fp]
         fp += dl.diff
     return frame_data
+
+
+def ref_loader(rel):
+    """The reference's DataLoader on data/<rel> (built with __new__: its
+    __init__ hard-codes /home/siri0005/..., quirk Q8), its own load_dataset,
+    and the frame dict restated from the CSV."""
+    sys.path.insert(0, REF)
+    import argParser
+    import load_traj
+
+    args = argParser.ArgsParser().parser.parse_args([])
+    d = os.path.join(REF, "data", rel)
+    csv = sorted(glob.glob(d + "*.csv"))[0]
+    dl = load_traj.DataLoader.__new__(load_traj.DataLoader)
+    dl.batch_size, dl.seq_length = args.batch_size, args.seq_length
+    dl.pred_len, dl.obs_len, dl.diff = args.pred_len, args.obs_len, args.obs_len
+    dl.infer = False
+    dl.current_dir = d
+    dl.load_dataset(csv)
+    dl.trajectories = frame_dict_from_csv(dl)
+    dl.num_batches = int((len(dl.frameList) / dl.seq_length) / dl.batch_size)
+    return dl, args
+
+
+def _pack(prefix, recs, out):
+    """Per-batch records -> flat arrays: scalars stacked, arrays concatenated
+    along axis 0 with a <field>_off offsets array, digests as strings."""
+    fields = []
+    for r in recs:
+        fields += [f for f in r if f not in fields]
+    out[prefix + "count"] = np.int64(len(recs))
+    for f in fields:
+        vals = [r.get(f) for r in recs]
+        if all(isinstance(v, str) or v is None for v in vals):
+            out[prefix + f] = np.array(["" if v is None else v for v in vals])
+        elif all(v is None or np.ndim(v) == 0 for v in vals):
+            out[prefix + f] = np.array([np.nan if v is None else v for v in vals], dtype=np.float64)
+        else:
+            arrs = [np.asarray(v) for v in vals if v is not None]
+            tail = arrs[0].shape[1:]
+            arrs = [np.zeros((0,) + tail) if v is None else np.asarray(v).reshape((-1,) + tail)
+                    for v in vals]
+            out[prefix + f] = np.concatenate(arrs, axis=0)
+            out[prefix + f + "_off"] = np.cumsum([0] + [len(a) for a in arrs]).astype(np.int64)
+
+
+SAMPLE_OFFSETS = (0, 5, 11)      # sample walks from seed + 8k (k = 0: sample.py itself)
+TRAIN_EPOCHS = 3
+
+
+def make_walk_fixture(name, rel):
+    """Full walks of the reference's data side over EVERY batch
+    (tools/ref_walks.py): the train.py training walk (3 epochs), the
+    validation walk from the data seed (--valid_from_seed) and from 0 (the
+    reference's own reset: no batch), and sample.py's walk from the seed and
+    from two shifted pointers.  Writes tests/golden/walk_<name>.npz."""
+    out = {}
+    dl, args = ref_loader(rel)
+    import networkx_graph
+    import ref_walks
+
+    recs, events = ref_walks.train_walk(dl, networkx_graph, args, TRAIN_EPOCHS)
+    _pack("tw_", recs, out)
+    out["tw_events"] = np.array([f"{ev[0]}:{ev[1]}" + (f":{ev[2]}" if len(ev) > 2 else "")
+                                 for ev in events])
+    for tag, start in (("vs_", dl.seed), ("v0_", 0)):
+        dl, args = ref_loader(rel)
+        recs, info = ref_walks.valid_walk(dl, networkx_graph, args, start)
+        _pack(tag, recs, out)
+        out[tag + "end"] = np.array(info["end"])
+        out[tag + "valid_num_batches"] = np.int64(info["valid_num_batches"])
+        out[tag + "valid_frame_pointer"] = np.int64(info["valid_frame_pointer"])
+    for k in SAMPLE_OFFSETS:
+        dl, args = ref_loader(rel)
+        recs = ref_walks.sample_walk(dl, networkx_graph, args, offset=k)
+        if k:                 # shifted walks: keys, counts and digests only
+            recs = [dict(b=r["b"], fp=r["fp"], keys=r["keys"], P=r["P"],
+                         npl_digest=ref_walks.digest(r["node_ids"], r["npl"]),
+                         tgt_digest=ref_walks.digest(r["node_tlens"], r["node_targets"]))
+                    for r in recs]
+        _pack(f"s{k}_", recs, out)
+    np.savez_compressed(os.path.join(OUT, f"walk_{name}.npz"), **out)
+    return {k: v.shape for k, v in out.items() if k.endswith("count")}
 
 
 def make_data_fixture(name, rel):
@@ -208,6 +292,7 @@ def main():
     for name, rel in DATASETS.items():
         rec = make_data_fixture(name, rel)
         print(name, {k: np.shape(v) for k, v in rec.items() if k.startswith("b0")})
+        make_walk_fixture(name, rel)
     print("checkpoint pairs (weight_c @ cost == stored Variable):", make_ckpt_fixture())
     print("gridlstm weights:", make_gridlstm_fixture())
     print("mcrAttn model copy:", make_ckpt_scope_fixture())
