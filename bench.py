@@ -51,27 +51,28 @@ REAL = "eth_ucy_real"          # config 3's workload on real data (multimodaltra
 # ---------------------------------------------------------------------------
 # algorithmic bytes: compulsory HBM traffic of one launch
 # ---------------------------------------------------------------------------
-def algorithmic_bytes(b, H, params_bytes):
+def algorithmic_bytes(b, H, params_bytes, targets_shared=False):
     """One g2k_step_fused_f32 launch: reads the ACTIVE pedestrians' positions
-    (W rows), vislet and targets (F frames x 24 floats), G, h_in, n_active and
-    the weights; writes pred for the active columns (padded columns are not
-    written), h_out and the metrics row."""
+    (W rows), vislet and targets (F frames x 24 floats; one frame's with
+    shared targets), G, h_in, n_active and the weights; writes pred for the
+    active pedestrians, h_out and the metrics row."""
     S, W, Nmax, _ = b.pos.shape
     L2, D, T = 24, 16, 8
     F = b.n_frames.astype(np.int64) if b.n_frames is not None else b.F
+    FT = np.minimum(F, 1) if targets_shared else F
     nact = b.n_active.astype(np.int64)
     extra = S * 4 + S * Nmax if b.n_frames is not None else 0      # n_frames, ped_mask
     rd = (W * nact * 8).sum() + (2 * nact * 4).sum() + S * D * T * 4 \
-        + (F * nact * L2 * 4).sum() + S * D * H * 4 + S * 4 + params_bytes + extra
+        + (FT * nact * L2 * 4).sum() + S * D * H * 4 + S * 4 + params_bytes + extra
     wr = (F * L2 * nact * 4).sum() + S * D * H * 4 + S * 8 * 4
     return int(rd + wr)
 
 
-def train_algorithmic_bytes(b, H, params_bytes, P):
+def train_algorithmic_bytes(b, H, params_bytes, P, targets_shared=False):
     """One train step (forward outputs + gradient + update): the forward's
     bytes, the [P + 2] gradient written and read back, the parameters and the
     RMSProp mean squares read and written once."""
-    return algorithmic_bytes(b, H, params_bytes) + 2 * (P + 2) * 4 + 4 * P * 4
+    return algorithmic_bytes(b, H, params_bytes, targets_shared) + 2 * (P + 2) * 4 + 4 * P * 4
 
 
 # ---------------------------------------------------------------------------
@@ -111,6 +112,23 @@ def _oracle_scenes(b, params_np, lo, hi, budget_s, threads):
         return frames, time.perf_counter() - t0
 
 
+def job_cpus():
+    """CPUs this job may use: the affinity mask, capped by a cgroup CPU quota
+    and by the job's declared CPU share (OMP_NUM_THREADS: the GPU box sets it
+    to the job's share of its host, 16 of 256 threads per GPU)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def _pool_worker(a):
     b, p, lo, hi, budget = a
     return _oracle_scenes(b, p, lo, hi, budget, 1)
@@ -129,17 +147,23 @@ def cpu_baseline(cfg, b, params_np, budget_s, procs):
     jobs = [(b, params_np, (i * per) % S, min(S, (i * per) % S + per), budget_s / 2)
             for i in range(procs)]
     ctx = mp.get_context("spawn")
-    with ctx.Pool(procs) as pool:
+    pool = ctx.Pool(procs)
+    try:
         res = pool.map(_pool_worker, jobs)
+    finally:
+        pool.close()          # let the workers exit on their own (no SIGTERM on teardown)
+        pool.join()
     agg = sum(f for f, _ in res) / max(t for _, t in res)
     return {"value": f1 / t1, "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": f"the float64 NumPy oracle (oracle/g2k_ref.py) in train.py's per-scene loop, "
                       f"{f1} frames of the same workload's scenes in {t1:.1f} s, "
                       f"1 thread (the reference's TF path cannot run here: no TF 1.x)",
-            "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "job_cpus": job_cpus(),
             "blas_all_threads": {"value": fa / ta, "unit": "frames/s", "seconds": round(ta, 2)},
             "all_core_aggregate": {"value": agg, "unit": "frames/s", "processes": procs,
-                                   "note": "disjoint scene slices, one BLAS thread each"}}
+                                   "note": "disjoint scene slices, one BLAS thread each, one "
+                                           "process per CPU this job may use (job_cpus; the "
+                                           "host's other threads belong to other jobs)"}}
 
 
 # ---------------------------------------------------------------------------
@@ -269,8 +293,12 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--cpu-procs", type=int, default=0,
-                    help="processes of the all-core CPU aggregate (0: min(16, cpu_count))")
+                    help="processes of the all-core CPU aggregate (0: the CPUs this job may use)")
     ap.add_argument("--no-train", action="store_true", help="skip the train-mode timing")
+    ap.add_argument("--pred-layout", choices=("ped", "band"), default="ped",
+                    help="pred as [S, F, Nmax, L, 2] (the per-pedestrian view train.py:254 "
+                         "transposes to; only active pedestrians written) or pred_path_band "
+                         "[S, F, 2L, Nmax]")
     ap.add_argument("--selftest-launcher", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 
@@ -300,7 +328,7 @@ def main(argv=None):
     # process initialises the GPU
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        procs = args.cpu_procs or job_cpus()
         cpu = cpu_baseline(args.config, b, params_host.numpy(), args.cpu_budget, procs)
 
     torch.cuda.set_device(local)
@@ -313,12 +341,16 @@ def main(argv=None):
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     params = params_host.to(dev)
     pbytes = sum(getattr(params, k).numel() * 4 for k in ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo"))
-    abytes = algorithmic_bytes(b, H, pbytes)
+    shared = args.config == REAL          # real scenes: one target set per scene (every frame's)
+    layout = dict(pred_layout=args.pred_layout, targets_shared=shared, frames=F if shared else None)
+    abytes = algorithmic_bytes(b, H, pbytes, shared)
     K = args.rotate or max(1, -(-MALL_BYTES // abytes) + 1)
 
     # K device-resident input batches (the base batch plus small per-batch
     # position offsets, so no two share a cache line) and their plans
     base = b.to_device(dev)
+    if shared:
+        base["targets"] = base["targets"][:, :1].contiguous()
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
     batches, plans = [], []
@@ -327,13 +359,13 @@ def main(argv=None):
         if k:
             t["pos"].add_(1e-3 * torch.randn(t["pos"].shape, device=dev, generator=gen))
             t["targets"].add_(1e-3 * torch.randn(t["targets"].shape, device=dev, generator=gen))
-        out = fs.StepOutputs(pred=torch.zeros((S, F, 24, Nmax), device=dev),
+        out = fs.StepOutputs(pred=torch.zeros(fs.pred_shape(S, F, Nmax, args.pred_layout), device=dev),
                              h=torch.empty((S, 16, H), device=dev),
                              metrics=torch.empty((S, 8), device=dev))
         batches.append(t)
         plans.append(fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"],
                                  t["n_active"], t["h0"], n_frames=t["n_frames"],
-                                 ped_mask=t["ped_mask"], stride=b.stride, out=out))
+                                 ped_mask=t["ped_mask"], stride=b.stride, out=out, **layout))
 
     def step(i):
         plans[i % K].run()
@@ -350,7 +382,7 @@ def main(argv=None):
 
     train = None
     if not args.no_train:
-        train = time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K)
+        train = time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, layout)
 
     if rank == 0:
         m = tot.cpu().numpy()
@@ -376,7 +408,8 @@ def main(argv=None):
                        "frames_per_scene": F if b.n_frames is None else float(b.n_frames.mean()),
                        "frames_per_step": b.frames, "obs_len": 8, "pred_len": 12, "Nmax": Nmax,
                        "hidden": H, "D": 16, "parallelism": f"dp{world}",
-                       "input_batches_rotated": K},
+                       "input_batches_rotated": K, "pred_layout": args.pred_layout,
+                       "targets_shared": shared},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": load_pmc(args.config),
@@ -398,7 +431,7 @@ def main(argv=None):
     return 0
 
 
-def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K):
+def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, layout):
     """--mode train: the same step plus loss gradient, ONE
     all-reduce of the flat [P + 2] gradient buffer across ranks (RCCL under
     the nccl backend) and the RMSProp update (multimodaltraj_2_amd/train_step.py).
@@ -406,7 +439,8 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K):
     from multimodaltraj_2_amd.train_step import TrainStep
     t0 = batches[0]
     ts = TrainStep(params, t0["pos"], t0["vislet"], t0["G"], t0["targets"], t0["n_active"],
-                   t0["h0"], n_frames=t0["n_frames"], ped_mask=t0["ped_mask"], stride=b.stride)
+                   t0["h0"], n_frames=t0["n_frames"], ped_mask=t0["ped_mask"], stride=b.stride,
+                   **layout)
     for t in batches[1:]:
         ts.bind(t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
                 n_frames=t["n_frames"], ped_mask=t["ped_mask"])
@@ -418,7 +452,7 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K):
     el = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
     gl = last["g"].double().cpu().numpy()
     kern_s = event_time(step, max(20, min(args.steps, 200)), torch.cuda.current_stream())
-    abytes = train_algorithmic_bytes(b, H, pbytes, ts.P)
+    abytes = train_algorithmic_bytes(b, H, pbytes, ts.P, layout["targets_shared"])
     achieved = abytes / kern_s / 1e9
     return {"metric": "frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + L2 loss gradient + "
                       "gradient all-reduce + RMSProp update",

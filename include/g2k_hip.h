@@ -53,7 +53,22 @@ typedef struct g2k_dims {
   int32_t Nmax;    /* padded pedestrians per scene                            */
   int32_t W;       /* position rows per scene, >= (F-1)*stride + T            */
   int32_t stride;  /* position-window advance per frame (1 sliding, 0 fixed)  */
+  int32_t flags;   /* G2K_STEP_* layout options of the fused step / train mode;
+                      0 for every other entry point                           */
 } g2k_dims;
+
+/* g2k_dims.flags (g2k_step_fused_f32, g2k_train_step_f32, g2k_step_grad_f32,
+ * g2k_step_grad_update_f32):
+ *   G2K_STEP_PRED_PED_MAJOR  pred is [S, F, Nmax, L, 2] (pedestrian-major: the
+ *     per-pedestrian view the reference's error loops index, pred_path
+ *     transposed, train.py:254; the targets' layout) instead of
+ *     pred_path_band [S, F, 2L, Nmax]; only pedestrians < n_active are
+ *     written (one contiguous n_active * 96-byte run per frame).
+ *   G2K_STEP_TARGETS_SHARED  targets is [S, 1, Nmax, L, 2]: one set for every
+ *     frame of a scene (the reference feeds a batch's targets to every frame
+ *     of its loop, train.py:197-276; real-data scenes). */
+#define G2K_STEP_PRED_PED_MAJOR 1
+#define G2K_STEP_TARGETS_SHARED 2
 
 /* Model parameters (device pointers). Shapes as in the reference. */
 typedef struct g2k_weights {
@@ -95,12 +110,14 @@ int64_t g2k_step_workspace_bytes(const g2k_dims* d);
  *   vislet   [S, 2, Nmax]          load_traj.py:139 rows 4:6 slice
  *   G        [S, D, T]             `_2dconv_in` feed (train.py:158, 232)
  *   targets  [S, F, Nmax, L, 2]    target assigned to each prediction row
+ *                                  ([S, 1, Nmax, L, 2] with G2K_STEP_TARGETS_SHARED)
  *   n_active [S] int32             pedestrians present (<= Nmax)
  *   n_frames [S] int32 or NULL     frames present (<= F); NULL = F
  *   ped_mask [S, Nmax] uint8 or NULL  rows with a target; NULL = all active
  *   h_in     [S, D, H]             hidden_state entering frame 0
  *   h_out    [S, D, H]             hidden_state after the last frame (may alias h_in)
- *   pred     [S, F, 2L, Nmax]      pred_path_band per frame (rows x then y); only
+ *   pred     [S, F, 2L, Nmax]      pred_path_band per frame (rows x then y) or, with
+ *                                  G2K_STEP_PRED_PED_MAJOR, [S, F, Nmax, L, 2]; only
  *                                  frames < n_frames and columns < min(Nmax,
  *                                  16 ceil(n_active / 16)) are written (whole
  *                                  16-column tiles: the columns past n_active 0)

@@ -22,7 +22,12 @@ c_vp = ctypes.c_void_p
 
 class G2KDims(ctypes.Structure):
     _fields_ = [("S", c_i32), ("F", c_i32), ("T", c_i32), ("L", c_i32), ("D", c_i32),
-                ("H", c_i32), ("Nmax", c_i32), ("W", c_i32), ("stride", c_i32)]
+                ("H", c_i32), ("Nmax", c_i32), ("W", c_i32), ("stride", c_i32),
+                ("flags", c_i32)]
+
+
+STEP_PRED_PED_MAJOR = 1      # g2k_dims.flags (include/g2k_hip.h)
+STEP_TARGETS_SHARED = 2
 
 
 class G2KWeights(ctypes.Structure):

@@ -33,8 +33,10 @@ namespace {
 // T, L fixed by the model (argParser.py:26-28, models/g2k_lstm_mcr.py:124);
 // D = 16 for the fused step and train mode (train.py:93), 1..16 for the
 // class-level forward and the recurrence (sample.py: num_freq_blocks = 10)
-int validate_common(const g2k_dims* d, bool need_F, bool any_D = false) {
+int validate_common(const g2k_dims* d, bool need_F, bool any_D = false, int flags_ok = 0) {
   if (!d) return set_err(G2K_EINVAL, "dims is NULL");
+  if (d->flags & ~flags_ok)
+    return set_err(G2K_EUNSUPPORTED, "flags 0x%x not supported by this entry point", d->flags);
   if (d->T != kT || d->L != kL)
     return set_err(G2K_EUNSUPPORTED, "unsupported geometry T=%d L=%d (need 8/12)", d->T, d->L);
   if (any_D ? (d->D < 1 || d->D > kD) : d->D != kD)
@@ -67,7 +69,7 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 int validate_step_inputs(const g2k_dims* d, const g2k_weights* w, const float* pos,
                          const float* vislet, const float* G, const float* targets,
                          const int32_t* n_active) {
-  int rc = validate_common(d, true);
+  int rc = validate_common(d, true, false, G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED);
   if (rc) return rc;
   if ((rc = validate_weights(w, true))) return rc;
   if (d->stride < 0) return set_err(G2K_EINVAL, "stride=%d < 0", d->stride);
@@ -135,13 +137,15 @@ int g2k_abi_version(void) { return G2K_ABI_VERSION; }
 
 const char* g2k_last_error(void) { return g_err; }
 
+constexpr int kStepFlags = G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED;
+
 int64_t g2k_step_lds_bytes(const g2k_dims* d) {
-  if (validate_common(d, true) != G2K_OK) return 0;
+  if (validate_common(d, true, false, kStepFlags) != G2K_OK) return 0;
   return scene_lds_bytes(d, false);
 }
 
 int64_t g2k_step_workspace_bytes(const g2k_dims* d) {
-  if (validate_common(d, true) != G2K_OK) return -1;
+  if (validate_common(d, true, false, kStepFlags) != G2K_OK) return -1;
   return 0;   // the fused step keeps every intermediate on chip
 }
 
@@ -168,7 +172,7 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
 }
 
 int64_t g2k_train_workspace_bytes(const g2k_dims* d) {
-  if (validate_common(d, true) != G2K_OK) return -1;
+  if (validate_common(d, true, false, kStepFlags) != G2K_OK) return -1;
   return grad_rows_bytes(d);
 }
 
@@ -208,6 +212,7 @@ int g2k_mcr_forward_f32(const g2k_dims* d, const g2k_weights* w, const float* X,
 int g2k_frame_recurrence_f32(const g2k_dims* d, const float* A, float* h, int32_t frames,
                              void* stream) {
   if (!d) return set_err(G2K_EINVAL, "dims is NULL");
+  if (d->flags) return set_err(G2K_EUNSUPPORTED, "flags must be 0");
   if (d->D < 1 || d->D > kD) return set_err(G2K_EUNSUPPORTED, "D=%d (1..16)", d->D);
   int rc = validate_H(d->H);
   if (rc) return rc;
@@ -271,12 +276,12 @@ int g2k_gridlstm_f32(const float* in, int64_t ld_in, const float* state, int64_t
 }
 
 int64_t g2k_grad_size(const g2k_dims* d) {
-  if (validate_common(d, false) != G2K_OK) return -1;
+  if (validate_common(d, false, false, kStepFlags) != G2K_OK) return -1;
   return grad_params(d->Nmax);
 }
 
 int64_t g2k_grad_workspace_bytes(const g2k_dims* d) {
-  if (validate_common(d, true) != G2K_OK) return -1;
+  if (validate_common(d, true, false, kStepFlags) != G2K_OK) return -1;
   return grad_rows_bytes(d);
 }
 
@@ -309,6 +314,7 @@ int g2k_step_grad_update_f32(const g2k_dims* d, const g2k_weights* w, const floa
 static int validate_nll(const g2k_dims* d, const float* pred, const float* head,
                         const int32_t* n_active) {
   if (!d) return set_err(G2K_EINVAL, "dims is NULL");
+  if (d->flags) return set_err(G2K_EUNSUPPORTED, "flags must be 0 (pred_path_band layout)");
   if (d->T != kT || d->L != kL) return set_err(G2K_EUNSUPPORTED, "T=%d L=%d (8, 12)", d->T, d->L);
   if (d->S < 0 || d->F < 0 || d->Nmax < 1 || d->Nmax > kMaxN)
     return set_err(G2K_EINVAL, "S=%d F=%d Nmax=%d", d->S, d->F, d->Nmax);

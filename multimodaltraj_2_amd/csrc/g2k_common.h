@@ -48,6 +48,11 @@ __device__ __forceinline__ brsrc make_brsrc(const void* base, uint32_t bytes) {
 __device__ __forceinline__ void bstore(brsrc r, int off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
+__device__ __forceinline__ void bstore4(brsrc r, int off, float a, float b, float c, float d) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
 __device__ __forceinline__ float4 bload4(brsrc r, int off) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
   return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),

@@ -47,7 +47,8 @@ constexpr int SM_SPARE = 1084;  // write-only word (stores of lanes without an e
 constexpr int kSceneSmall = 1088;
 constexpr int kKA = 12;       // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
 constexpr int kYP = 17;       // train: per-producer dY tile scratch [24][kYP] (pitch: bank spread)
-constexpr int kTileStores = 8;   // global stores per prediction tile (4-byte path)
+// global stores per prediction tile: pred_path_band (4-byte path) / pedestrian-major (16-byte)
+template <bool PM> constexpr int tile_stores() { return PM ? 2 : 8; }
 // train mode
 constexpr int kGFrame = 192;  // per-producer frame scratch: dM [24][8] (frame_grad's P6)
 constexpr int kGT_DM = 0;
@@ -304,6 +305,7 @@ struct SceneCtx {
   int* sGseq;     // train: [0] producers done with the chunk's frames (cumulative), [2 + t]
                   // frames added to dWo tile t (dwo_seq)
   int s, tid, lane, wv, L, q, nact, nf, ntiles, ntact;
+  int tfs;        // 1: targets per frame; 0: one set for all frames (G2K_STEP_TARGETS_SHARED)
 };
 
 // LDS-DMA of a chunk's position window rows (train.py:76-79 window) into
@@ -577,7 +579,7 @@ __device__ __forceinline__ int mrow(int r) { return (r & 1) * kL + (r >> 1); }
 // `after_targets` runs once the target registers are consumed (GRAD: the
 // next tile's targets are loaded into them there, before this tile's stores,
 // so the next tile's wait counts exactly those stores).
-template <bool GRAD, typename AfterTargets>
+template <bool GRAD, bool PM, typename AfterTargets>
 __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, brsrc pr,
                                           const float2 (&tg)[4], bool has_t, int Nmax, int nact,
                                           int t, int L, int q, float acc[5], float& lsum,
@@ -615,7 +617,15 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
   }
   after_targets();
   asm volatile("" ::: "memory");                           // ... then the stores
-  {
+  if (PM) {
+    // pedestrian-major [Nmax][L][2]: the lane's Y values ARE its target row's
+    // floats 4q..4q+3 and 16+4q..16+4q+3 (r = 2 step + xy), so two 16-byte
+    // stores at the offsets of its two target loads; pedestrians >= n_active
+    // are not written (a contiguous n_active * 96-byte run per frame)
+    const int off = n * kL2 * 4;
+    bstore4(pr, n < nact ? off + 16 * q : kBufOff, y0[0], y0[1], y0[2], y0[3]);
+    bstore4(pr, (n < nact && hi) ? off + 64 + 16 * q : kBufOff, y1[0], y1[1], y1[2], y1[3]);
+  } else {
     // range-checked 4-byte stores (no branch): the block-1 rows of lane
     // groups 2, 3 and columns past Nmax fall outside the frame's buffer.  The
     // tile's 16 columns are written whole (Y = 0 past n_active, w = 0 there):
@@ -956,11 +966,12 @@ __device__ __forceinline__ int grad_rec_frames(int cnt, int NP) { return cnt >= 
 // 16 t + L, floats 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row, zero
 // for q >= 2) by range-checked buffer loads (no branch: !ok and inactive
 // pedestrians n >= n_active read zeros without touching memory).
+// tfs = 0: one target set for every frame (G2K_STEP_TARGETS_SHARED).
 __device__ __forceinline__ void load_targets(brsrc tgr, int Nmax, int nact, int fb, int fl, int t,
-                                             bool ok, int L, int q, float2 (&tg)[4]) {
+                                             bool ok, int L, int q, float2 (&tg)[4], int tfs) {
   const int ne = 16 * t + L;
   ok = ok && ne < nact;
-  const int base = (((fb + fl) * Nmax + (ne < Nmax ? ne : 0)) * kL2) * 4;
+  const int base = ((((fb + fl) & -tfs) * Nmax + (ne < Nmax ? ne : 0)) * kL2) * 4;
   // two 16-B loads (rows are 96 B: every float4 is 16-B aligned)
   const float4 u = bload4(tgr, ok ? base + 16 * q : kBufOff);
   const float4 w = bload4(tgr, ok && q < 2 ? base + 64 + 16 * q : kBufOff);
@@ -971,19 +982,23 @@ __device__ __forceinline__ void load_targets(brsrc tgr, int Nmax, int nact, int 
 }
 
 __device__ __forceinline__ brsrc scene_targets_rsrc(const StepArgs& a, int s) {
-  return make_brsrc(a.targets + (size_t)s * a.d.F * a.d.Nmax * kL2,
-                    (uint32_t)a.d.F * a.d.Nmax * kL2 * 4);
+  const int tf = (a.d.flags & G2K_STEP_TARGETS_SHARED) ? 1 : a.d.F;   // target frames per scene
+  return make_brsrc(a.targets + (size_t)s * tf * a.d.Nmax * kL2, (uint32_t)tf * a.d.Nmax * kL2 * 4);
 }
 
-// kTileStores out-of-range stores right after the first target load of a
+// tile_stores out-of-range stores right after the first target load of a
 // tile loop: every wait on a target load in the loop then has the same number
 // of younger stores before it (a tile's own) and the compiler's counts stay
-// exact (vmcnt(kTileStores), not 0).
+// exact (vmcnt(tile_stores), not 0).
+template <bool PM>
 __device__ __forceinline__ void balance_stores(const StepArgs& a) {
   asm volatile("" ::: "memory");
   const brsrc none = make_brsrc(a.targets, 0u);
 #pragma unroll
-  for (int i = 0; i < kTileStores; ++i) bstore(none, kBufOff, 0.f);
+  for (int i = 0; i < tile_stores<PM>(); ++i) {
+    if (PM) bstore4(none, kBufOff, 0.f, 0.f, 0.f, 0.f);
+    else bstore(none, kBufOff, 0.f);
+  }
 }
 
 // GRAD: one gradient worker's frames fl = f0, f0 + fstep, ... < fend of the
@@ -994,6 +1009,7 @@ __device__ __forceinline__ void balance_stores(const StepArgs& a) {
 // each tile loads the next tile's targets as soon as its own are consumed,
 // before its prediction stores (tg holds the first tile's targets on entry
 // when `preloaded`).
+template <bool PM>
 __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int slot, int fb, int f0, int fstep,
                                             int fend, unsigned act_bits, float (&acc)[5],
@@ -1001,8 +1017,8 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
   const int Nmax = a.d.Nmax, F = a.d.F, L = c.L, q = c.q, ntact = c.ntact;
   const brsrc tgr = scene_targets_rsrc(a, c.s);
   if (!preloaded) {
-    load_targets(tgr, Nmax, c.nact, fb, f0, 0, f0 < fend, L, q, tg);
-    balance_stores(a);
+    load_targets(tgr, Nmax, c.nact, fb, f0, 0, f0 < fend, L, q, tg, c.tfs);
+    balance_stores<PM>(a);
   }
   float* ys = c.sY + slot * kL2 * kYP;
   f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -1015,9 +1031,9 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
       const bool nxt = t + 1 < ntact;                    // the next tile: this frame's, else the next frame's
       const int nfl = nxt ? fl : fl + fstep, nt = nxt ? t + 1 : 0;
       f32x4 dWoT;
-      pred_tile<true>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
-                      c.nact, t, L, q, acc, lsum, dm, dWoT,
-                      [&] { load_targets(tgr, Nmax, c.nact, fb, nfl, nt, nfl < fend, L, q, tg); });
+      pred_tile<true, PM>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
+                          c.nact, t, L, q, acc, lsum, dm, dWoT,
+                          [&] { load_targets(tgr, Nmax, c.nact, fb, nfl, nt, nfl < fend, L, q, tg, c.tfs); });
       // dWo^T[n0 + 4q + v][t = L]: one copy per worker, or one copy added
       // to in frame order (tile sequence word) when that is too big
       const int nb = 16 * t + 4 * q;
@@ -1084,7 +1100,7 @@ __device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCt
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
-template <int NP, bool GRAD>
+template <int NP, bool GRAD, bool PM>
 __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLayout& lay,
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
@@ -1107,7 +1123,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     const bool ok = k < nitems;
     int fl, t;
     item_ft(ok ? k : 0, fl, t);
-    load_targets(tgr, Nmax, c.nact, fb, fl, t, ok, L, q, tg);
+    load_targets(tgr, Nmax, c.nact, fb, fl, t, ok, L, q, tg, c.tfs);
   };
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float lsum = 0.f;
@@ -1123,8 +1139,8 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // the first tiles' targets: in flight during the heads (GRAD: one buffer
     // and the balancing stores, see grad_frames)
     if (GRAD) {
-      load_targets(tgr, Nmax, c.nact, fb, pw, 0, pw < gend, L, q, tgA);
-      balance_stores(a);
+      load_targets(tgr, Nmax, c.nact, fb, pw, 0, pw < gend, L, q, tgA, c.tfs);
+      balance_stores<PM>(a);
     } else {
       load_item(fb, nitems, 0, tgA);
       load_item(fb, nitems, 1, tgB);
@@ -1164,7 +1180,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     }
     // phase 2 — predictions and errors (GRAD: and the gradient)
     if (GRAD) {
-      grad_frames(a, lay, c, pw, fb, pw, NP, gend, act_bits, acc, lsum, tgA, true);
+      grad_frames<PM>(a, lay, c, pw, fb, pw, NP, gend, act_bits, acc, lsum, tgA, true);
       // every worker done with the chunk's frames -> its dU rows into dV
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) atomicAdd(c.sGseq, 1);
@@ -1180,8 +1196,8 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
         const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : a.targets,
                                     a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
         f32x4 dWoT;
-        pred_tile<false>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tg, (act_bits >> t) & 1u, Nmax,
-                         c.nact, t, L, q, acc, lsum, dm, dWoT, [] {});
+        pred_tile<false, PM>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tg, (act_bits >> t) & 1u,
+                             Nmax, c.nact, t, L, q, acc, lsum, dm, dWoT, [] {});
       };
       for (int k = 0; k < nitems; k += 2) {
         item(k, tgA);
@@ -1300,7 +1316,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
 // GRAD, recurrence wave w after its recurrence: the last R frames of the
 // last chunk (frame cnt - R + w) as gradient worker NP + w, then its metrics
 // row and ticket (with zero partials when R = 0).
-template <int NP>
+template <int NP, bool PM>
 __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayout& lay,
                                               const SceneCtx& c) {
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1311,8 +1327,8 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
     const int R = grad_rec_frames(cnt, NP);
     if (R > 0) {
       float2 tg[4];
-      grad_frames(a, lay, c, NP + c.wv, fb, cnt - R + c.wv, R, cnt, scene_act_bits(a, c), acc, lsum,
-                  tg, false);
+      grad_frames<PM>(a, lay, c, NP + c.wv, fb, cnt - R + c.wv, R, cnt, scene_act_bits(a, c), acc,
+                      lsum, tg, false);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (c.lane == 0) atomicAdd(c.sGseq, 1);
     }
@@ -1320,7 +1336,7 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
   publish_metrics(a, c, NP + c.wv, NP + kRecW, acc, lsum, true);
 }
 
-template <int TPW, int NP, bool GRAD>
+template <int TPW, int NP, bool GRAD, bool PM>
 __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   constexpr int NT = 64 * (kRecW + NP);
   constexpr int kRB = 16 * kRecW;
@@ -1402,12 +1418,13 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     c.nf = a.n_frames ? clampi(nf, 0, F) : F;
   }
   c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians
+  c.tfs = (a.d.flags & G2K_STEP_TARGETS_SHARED) ? 0 : 1;
   if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
   if (c.wv < kRecW) {
     scene_recurrence<TPW, NP>(a, lay, c);
-    if (GRAD) rec_grad_work<NP>(a, lay, c);
+    if (GRAD) rec_grad_work<NP, PM>(a, lay, c);
   } else
-    scene_producer<NP, GRAD>(a, lay, c);
+    scene_producer<NP, GRAD, PM>(a, lay, c);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
 }
 
@@ -1428,8 +1445,12 @@ int scene_producers(int H, int Nmax, bool grad) {
 
 template <int TPW, int NP, bool GRAD>
 void launch_k(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
-  hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD>), dim3(a.d.S), dim3(64 * (kRecW + NP)),
-                     (size_t)l.total * 4, st, a, l);
+  if (a.d.flags & G2K_STEP_PRED_PED_MAJOR)
+    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, true>), dim3(a.d.S), dim3(64 * (kRecW + NP)),
+                       (size_t)l.total * 4, st, a, l);
+  else
+    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, false>), dim3(a.d.S), dim3(64 * (kRecW + NP)),
+                       (size_t)l.total * 4, st, a, l);
 }
 
 template <bool GRAD>

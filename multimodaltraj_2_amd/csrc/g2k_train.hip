@@ -139,6 +139,11 @@ __global__ void __launch_bounds__(64 * kRowSlices) g2k_grad_rows_kernel(const fl
            (int)gridDim.x - 1;
   __syncthreads();
   if (!last) return;
+  // the acquire side of the hand-off, in the last workgroup only (once per
+  // step): the other workgroups' gradient columns happen-before its loads
+  // under the HIP memory model, not just by gfx950's store ordering (their
+  // write-through stores completed, vmcnt(0), before their ticket increments)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   update_body<true>(up.params, up.ms, grad, width - 2, up.lr, up.decay, up.clip, &red[0][0]);
 }
 

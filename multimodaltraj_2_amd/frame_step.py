@@ -92,9 +92,31 @@ def _stream(stream):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+def step_flags(pred_layout="band", targets_shared=False) -> int:
+    """g2k_dims.flags: pred_layout "band" = pred_path_band [S, F, 2L, Nmax],
+    "ped" = pedestrian-major [S, F, Nmax, L, 2]; targets_shared = one
+    [S, 1, Nmax, L, 2] target set for every frame."""
+    if pred_layout not in ("band", "ped"):
+        raise ValueError(f"pred_layout {pred_layout!r}: 'band' or 'ped'")
+    return ((_lib.STEP_PRED_PED_MAJOR if pred_layout == "ped" else 0)
+            | (_lib.STEP_TARGETS_SHARED if targets_shared else 0))
+
+
+def pred_shape(S, F, Nmax, pred_layout="band"):
+    return (S, F, 2 * PRED_LEN, Nmax) if pred_layout == "band" else (S, F, Nmax, PRED_LEN, 2)
+
+
+def pred_band(pred, pred_layout="band"):
+    """Either layout -> pred_path_band [S, F, 2L, Nmax] (a view or a copy)."""
+    if pred_layout == "band":
+        return pred
+    S, F, N = pred.shape[:3]
+    return pred.permute(0, 1, 4, 3, 2).reshape(S, F, 2 * PRED_LEN, N)
+
+
 @dataclass
 class StepOutputs:
-    pred: torch.Tensor       # [S, F, 2L, Nmax]
+    pred: torch.Tensor       # [S, F, 2L, Nmax] (pred_layout "ped": [S, F, Nmax, L, 2])
     h: torch.Tensor          # [S, D, H]
     metrics: torch.Tensor    # [S, 8]
     attn: torch.Tensor | None = None   # [S, F, D, D]
@@ -129,16 +151,19 @@ def _workspace(nbytes, device):
 
 def step_fused(params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
                ped_mask=None, stride=1, lam=LAMBDA, out: StepOutputs | None = None,
-               want_attn=False, stream=None, h_out=None) -> StepOutputs:
+               want_attn=False, stream=None, h_out=None, pred_layout="band",
+               targets_shared=False, frames=None) -> StepOutputs:
     """One pass of the per-frame body of train.py:197-276 over S scenes.
 
     pos [S, W, Nmax, 2], vislet [S, 2, Nmax], G [S, D, T],
-    targets [S, F, Nmax, L, 2], n_active [S] int32, h [S, D, H].
-    ``F`` is taken from ``targets``.  Returns pred/h/metrics (and per-frame
-    attn / cost when ``want_attn``)."""
+    targets [S, F, Nmax, L, 2] (targets_shared: [S, 1, Nmax, L, 2] and F =
+    ``frames``), n_active [S] int32, h [S, D, H].  ``F`` is taken from
+    ``targets`` otherwise.  Returns pred (``pred_layout``, see step_flags) /
+    h / metrics (and per-frame attn / cost when ``want_attn``)."""
     plan = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
                     ped_mask=ped_mask, stride=stride, lam=lam, out=out, want_attn=want_attn,
-                    stream=stream, h_out=h_out)
+                    stream=stream, h_out=h_out, pred_layout=pred_layout,
+                    targets_shared=targets_shared, frames=frames)
     plan.run()
     return plan.out
 
@@ -152,10 +177,11 @@ class StepPlan:
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
                  n_frames=None, ped_mask=None, stride=1, lam=LAMBDA,
-                 out: StepOutputs | None = None, want_attn=False, stream=None, h_out=None):
+                 out: StepOutputs | None = None, want_attn=False, stream=None, h_out=None,
+                 pred_layout="band", targets_shared=False, frames=None):
         self._fn, self._args, self.out, self._keep = _prepare_step(
             params, pos, vislet, G, targets, n_active, h, n_frames, ped_mask, stride, lam, out,
-            want_attn, stream, h_out)
+            want_attn, stream, h_out, pred_layout, targets_shared, frames)
 
     def run(self) -> StepOutputs:
         rc = self._fn(*self._args)
@@ -164,8 +190,18 @@ class StepPlan:
         return self.out
 
 
+def step_frames(targets, targets_shared, frames):
+    """F of a step: targets.shape[1], or ``frames`` with shared targets."""
+    if not targets_shared:
+        return int(targets.shape[1])
+    if frames is None:
+        raise ValueError("targets_shared needs frames (F)")
+    return int(frames)
+
+
 def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_mask, stride, lam,
-                  out, want_attn, stream, h_out):
+                  out, want_attn, stream, h_out, pred_layout="band", targets_shared=False,
+                  frames=None):
     lib = _lib.load()
     dev = pos.device
     if dev.type != "cuda":
@@ -173,13 +209,14 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
     S, W, Nmax, two = pos.shape
     if two != 2:
         raise ValueError(f"pos: last dim {two}, expected 2")
-    F = int(targets.shape[1])
+    flags = step_flags(pred_layout, targets_shared)
+    F = step_frames(targets, targets_shared, frames)
     H = int(h.shape[2])
     params.check(dev)
     if params.nmax != Nmax:
         raise ValueError(f"params Nmax={params.nmax} but pos Nmax={Nmax}")
     exp = dict(pos=(S, W, Nmax, 2), vislet=(S, 2, Nmax), G=(S, HIDDEN_LEN, OBS_LEN),
-               targets=(S, F, Nmax, PRED_LEN, 2), h=(S, HIDDEN_LEN, H))
+               targets=(S, 1 if targets_shared else F, Nmax, PRED_LEN, 2), h=(S, HIDDEN_LEN, H))
     for k, t in dict(pos=pos, vislet=vislet, G=G, targets=targets, h=h).items():
         if tuple(t.shape) != exp[k]:
             raise ValueError(f"{k}: shape {tuple(t.shape)}, expected {exp[k]}")
@@ -197,14 +234,17 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
         # the kernel writes pred for frames < n_frames and columns < n_active
         # only: the rest stays as allocated (zero)
         out = StepOutputs(
-            pred=torch.zeros((S, F, 2 * PRED_LEN, Nmax), device=dev, dtype=torch.float32),
+            pred=torch.zeros(pred_shape(S, F, Nmax, pred_layout), device=dev, dtype=torch.float32),
             h=h_out if h_out is not None else torch.empty_like(h),
             metrics=torch.empty((S, 8), device=dev, dtype=torch.float32),
             attn=(torch.empty((S, F, HIDDEN_LEN, HIDDEN_LEN), device=dev, dtype=torch.float32)
                   if want_attn else None),
             cost=(torch.empty((S, F, OBS_LEN, OBS_LEN), device=dev, dtype=torch.float32)
                   if want_attn else None))
-    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride)
+    if tuple(out.pred.shape) != pred_shape(S, F, Nmax, pred_layout):
+        raise ValueError(f"out.pred: shape {tuple(out.pred.shape)}, expected "
+                         f"{pred_shape(S, F, Nmax, pred_layout)} ({pred_layout})")
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride, flags)
     w = params.abi()
     nws = int(lib.g2k_step_workspace_bytes(ctypes.byref(d)))
     if nws < 0:

@@ -24,7 +24,7 @@ import torch.distributed as dist
 from . import _lib
 from .dist import allreduce_grad
 from .frame_step import (HIDDEN_LEN, LAMBDA, OBS_LEN, PRED_LEN, G2KParams, StepPlan, _check_dev,
-                         _ptr, _stream)
+                         _ptr, _stream, step_flags, step_frames)
 
 GRAD_ORDER = ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo")   # g2k_weights order
 LEARNING_RATE = 0.005    # argParser.py:43
@@ -55,7 +55,8 @@ class GradPlan:
     ``run()`` returns grad [P + 2] = (gradient sums, loss, count)."""
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, *, n_frames=None,
-                 ped_mask=None, stride=1, lam=LAMBDA, grad=None, stream=None):
+                 ped_mask=None, stride=1, lam=LAMBDA, grad=None, stream=None,
+                 targets_shared=False, frames=None):
         lib = _lib.load()
         dev = pos.device
         if dev.type != "cuda":
@@ -63,12 +64,12 @@ class GradPlan:
         S, W, Nmax, two = pos.shape
         if two != 2:
             raise ValueError(f"pos: last dim {two}, expected 2")
-        F = int(targets.shape[1])
+        F = step_frames(targets, targets_shared, frames)
         params.check(dev)
         if params.nmax != Nmax:
             raise ValueError(f"params Nmax={params.nmax} but pos Nmax={Nmax}")
         exp = dict(pos=(S, W, Nmax, 2), vislet=(S, 2, Nmax), G=(S, HIDDEN_LEN, OBS_LEN),
-                   targets=(S, F, Nmax, PRED_LEN, 2))
+                   targets=(S, 1 if targets_shared else F, Nmax, PRED_LEN, 2))
         for k, t in dict(pos=pos, vislet=vislet, G=G, targets=targets).items():
             if tuple(t.shape) != exp[k]:
                 raise ValueError(f"{k}: shape {tuple(t.shape)}, expected {exp[k]}")
@@ -78,7 +79,8 @@ class GradPlan:
             _check_dev("n_frames", n_frames, dev, torch.int32)
         if ped_mask is not None:
             _check_dev("ped_mask", ped_mask, dev, torch.uint8)
-        d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 64, Nmax, W, stride)
+        d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 64, Nmax, W, stride,
+                         step_flags("band", targets_shared))
         P = int(lib.g2k_grad_size(ctypes.byref(d)))
         nws = int(lib.g2k_grad_workspace_bytes(ctypes.byref(d)))
         if P < 0 or nws < 0:
@@ -140,14 +142,17 @@ class TrainPlan:
     gradient rows summed in a fixed order, and optionally the update."""
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
-                 ped_mask=None, stride=1, lam=LAMBDA, out=None, grad=None, stream=None):
+                 ped_mask=None, stride=1, lam=LAMBDA, out=None, grad=None, stream=None,
+                 pred_layout="band", targets_shared=False, frames=None):
         lib = _lib.load()
         self.fwd = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
-                            ped_mask=ped_mask, stride=stride, lam=lam, out=out, stream=stream)
+                            ped_mask=ped_mask, stride=stride, lam=lam, out=out, stream=stream,
+                            pred_layout=pred_layout, targets_shared=targets_shared, frames=frames)
         dev = pos.device
         S, W, Nmax, _ = pos.shape
-        F, H = int(targets.shape[1]), int(h.shape[2])
-        d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride)
+        F, H = step_frames(targets, targets_shared, frames), int(h.shape[2])
+        d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride,
+                         step_flags(pred_layout, targets_shared))
         self.P = int(lib.g2k_grad_size(ctypes.byref(d)))
         nws = int(lib.g2k_train_workspace_bytes(ctypes.byref(d)))
         if self.P < 0 or nws < 0:
@@ -197,7 +202,9 @@ class TrainStep:
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
                  lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,
-                 n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None):
+                 n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None,
+                 pred_layout="band", targets_shared=False, frames=None):
+        self._layout = dict(pred_layout=pred_layout, targets_shared=targets_shared, frames=frames)
         self.flat, self.params = flat_params(params)
         self.P = self.flat.numel()
         self.ms = torch.ones_like(self.flat) if rmsprop else None
@@ -215,7 +222,7 @@ class TrainStep:
         """Bind another input batch; returns its slot for ``run``."""
         self._slots.append(TrainPlan(self.params, pos, vislet, G, targets, n_active, h,
                                      n_frames=n_frames, ped_mask=ped_mask, stride=self._stride,
-                                     lam=self._lam, out=out))
+                                     lam=self._lam, out=out, **self._layout))
         return len(self._slots) - 1
 
     @property

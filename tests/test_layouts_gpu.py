@@ -1,0 +1,100 @@
+"""GPU: the fused step's layout options (g2k_dims.flags, include/g2k_hip.h).
+
+G2K_STEP_PRED_PED_MAJOR writes pred as [S, F, Nmax, L, 2] — the per-pedestrian
+view train.py:254 transposes pred_path_band into — and only the active
+pedestrians; G2K_STEP_TARGETS_SHARED reads one [S, 1, Nmax, L, 2] target set
+for every frame (real-data scenes: the reference feeds a batch's targets to
+every frame of its loop).  Both must give bit-identical results to the
+default layouts (same arithmetic, other addresses), forward and train mode;
+the oracle parity of the default layouts is in test_step_gpu / test_train_gpu."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from multimodaltraj_2_amd import _lib
+from multimodaltraj_2_amd import frame_step as fs
+from multimodaltraj_2_amd import train_step as ts
+from multimodaltraj_2_amd.synthetic import make_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("Nmax,H", [(32, 128), (64, 256), (256, 256), (20, 64)])
+def test_ped_major_pred_equals_band(gpu, Nmax, H):
+    b = make_batch(24, Nmax, H, seed=5)
+    t = b.to_device(gpu)
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    ref = fs.step_fused(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+    out = fs.StepOutputs(pred=torch.full(fs.pred_shape(b.S, b.F, Nmax, "ped"), float("nan"), device=gpu),
+                         h=torch.empty_like(t["h0"]), metrics=torch.empty((b.S, 8), device=gpu))
+    got = fs.step_fused(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
+                        pred_layout="ped", out=out)
+    torch.cuda.synchronize()
+    band = fs.pred_band(got.pred, "ped").cpu().numpy()
+    want = ref.pred.cpu().numpy()
+    for s in range(b.S):
+        n = int(b.n_active[s])
+        np.testing.assert_array_equal(band[s, :, :, :n], want[s, :, :, :n])
+        assert np.isnan(got.pred[s, :, n:].cpu().numpy()).all()      # inactive: not written
+    np.testing.assert_array_equal(got.h.cpu().numpy(), ref.h.cpu().numpy())
+    np.testing.assert_array_equal(got.metrics.cpu().numpy(), ref.metrics.cpu().numpy())
+
+
+def _shared_batch(gpu, S=32, Nmax=32, H=128, F=9):
+    """Stride-0 scenes whose targets are the same in every frame."""
+    b = make_batch(S, Nmax, H, F=F, seed=9)
+    t = b.to_device(gpu)
+    t["pos"] = t["pos"][:, :8].contiguous()
+    t["targets1"] = t["targets"][:, :1].contiguous()
+    t["targets"] = t["targets1"].expand(-1, F, -1, -1, -1).contiguous()
+    t["n_frames"] = torch.from_numpy(np.random.default_rng(2).integers(0, F + 1, S).astype(np.int32)).to(gpu)
+    return b, t, F
+
+
+def test_shared_targets_equal_replicated(gpu):
+    b, t, F = _shared_batch(gpu)
+    params = fs.init_params(32, seed=0, device=gpu)
+    kw = dict(n_frames=t["n_frames"], stride=0)
+    ref = fs.step_fused(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
+                        **kw)
+    got = fs.step_fused(params, t["pos"], t["vislet"], t["G"], t["targets1"], t["n_active"], t["h0"],
+                        targets_shared=True, frames=F, **kw)
+    torch.cuda.synchronize()
+    for k in ("pred", "h", "metrics"):
+        np.testing.assert_array_equal(getattr(got, k).cpu().numpy(), getattr(ref, k).cpu().numpy())
+
+
+@pytest.mark.parametrize("layout,shared", [("ped", False), ("band", True), ("ped", True)])
+def test_train_step_layouts_equal_default(gpu, layout, shared):
+    b, t, F = _shared_batch(gpu)
+    kw = dict(n_frames=t["n_frames"], stride=0)
+    grads, preds = [], []
+    for lay, sh in (("band", False), (layout, shared)):
+        params = fs.init_params(32, seed=0, device=gpu)
+        tgt = t["targets1"] if sh else t["targets"]
+        tp = ts.TrainPlan(params, t["pos"], t["vislet"], t["G"], tgt, t["n_active"], t["h0"],
+                          pred_layout=lay, targets_shared=sh, frames=F if sh else None, **kw)
+        g = tp.run().clone()
+        gp = ts.GradPlan(params, t["pos"], t["vislet"], t["G"], tgt, t["n_active"],
+                         targets_shared=sh, frames=F if sh else None, **kw).run()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(g.cpu().numpy(), gp.cpu().numpy())
+        grads.append(g.cpu().numpy())
+        preds.append(fs.pred_band(tp.out.pred, lay).cpu().numpy())
+    np.testing.assert_array_equal(grads[0], grads[1])
+    for s in range(b.S):
+        n = int(b.n_active[s])
+        np.testing.assert_array_equal(preds[0][s, :, :, :n], preds[1][s, :, :, :n])
+
+
+def test_flags_rejected_where_unsupported(gpu):
+    lib = _lib.load()
+    d = _lib.G2KDims(1, 1, 8, 12, 16, 64, 8, 8, 0, _lib.STEP_PRED_PED_MAJOR)
+    x = torch.zeros(4096, device=gpu)
+    rc = lib.g2k_ade_fde_f32(ctypes.byref(d), x.data_ptr(), x.data_ptr(), x.data_ptr(), None, None,
+                             0, x.data_ptr(), None)
+    assert rc == -4 and b"flags" in lib.g2k_last_error()
+    d.flags = 8
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(d)) == -1

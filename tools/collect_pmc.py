@@ -10,11 +10,22 @@ mode "train": g2k_scene_kernel<..., true> + g2k_grad_rows_kernel + g2k_update_ke
               (one g2k_train_step_f32)
 
 usage: collect_pmc.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON MODE"""
-import collections, csv, glob, json, os, sys
+import collections, csv, glob, json, os, re, sys
 
-MODES = {"ref": (("g2k_scene_kernel<", ", false>"),),
-         "train": (("g2k_scene_kernel<", ", true>"), ("g2k_grad_rows_kernel", ""),
-                   ("g2k_update_kernel", ""))}
+SCENE = re.compile(r"g2k_scene_kernel<\s*\d+,\s*\d+,\s*(true|false)")
+
+
+def kernel_of(name, mode):
+    """The bench kernel a trace row belongs to in this mode, or None: the
+    scene kernel's third template argument is GRAD (false: reference mode)."""
+    m = SCENE.search(name)
+    if m:
+        return "g2k_scene_kernel" if (m.group(1) == "true") == (mode == "train") else None
+    if mode == "train":
+        for k in ("g2k_grad_rows_kernel", "g2k_update_kernel"):
+            if k in name:
+                return k
+    return None
 
 
 def per_kernel(d, counter, mode):
@@ -23,10 +34,9 @@ def per_kernel(d, counter, mode):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            k = r["Kernel_Name"]
-            for a, b in MODES[mode]:
-                if a in k and b in k:
-                    vals[a.rstrip("<")].append(float(r["Counter_Value"]))
+            k = kernel_of(r["Kernel_Name"], mode)
+            if k:
+                vals[k].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items() if v}
 
 
