@@ -69,6 +69,11 @@ typedef struct g2k_dims {
  *     of its loop, train.py:197-276; real-data scenes). */
 #define G2K_STEP_PRED_PED_MAJOR 1
 #define G2K_STEP_TARGETS_SHARED 2
+/* train mode only: the loss is the bivariate-Gaussian NLL of the prediction
+ * pairs around pred with the per-step head w->head (g2k_nll_f32's terms)
+ * instead of 1/2 the squared error; the gradient then covers the head too
+ * (P = 24 Nmax + 496 + 36, the head's 36 after Wo). */
+#define G2K_STEP_LOSS_NLL 4
 
 /* Model parameters (device pointers). Shapes as in the reference. */
 typedef struct g2k_weights {
@@ -79,6 +84,8 @@ typedef struct g2k_weights {
   const float* Wr;   /* [T, 2]     krnl_embed/weight_r     g2k_lstm_mcr.py:72   */
   const float* Wc;   /* [2L, T]    krnl_weights/weight_c   g2k_lstm_mcr.py:65   */
   const float* Wo;   /* [T, Nmax]  krnl_weights/weight_o   g2k_lstm_mcr.py:61   */
+  const float* head; /* [3, L] NLL head {log sigma_x, log sigma_y, atanh rho} per
+                        step, train mode with G2K_STEP_LOSS_NLL only (else NULL) */
 } g2k_weights;
 
 int g2k_abi_version(void);
@@ -217,9 +224,9 @@ int g2k_gridlstm_f32(const float* in, int64_t ld_in, const float* state, int64_t
  * pred_path_band against `targets` over frames < n_frames and the active,
  * masked pedestrians (the pairs the a9 errors use).
  *
- * g2k_grad_size: floats P in one parameter vector = 24*Nmax + 496, laid out
- *   in g2k_weights order (Wi, Wii, Wv, bv, Wr, Wc, Wo; padded shapes); -1 on
- *   invalid dims.
+ * g2k_grad_size: floats P in one parameter vector = 24*Nmax + 496 (+ 36 with
+ *   G2K_STEP_LOSS_NLL), laid out in g2k_weights order (Wi, Wii, Wv, bv, Wr, Wc,
+ *   Wo[, head]; padded shapes); -1 on invalid dims.
  * g2k_grad_workspace_bytes: device workspace g2k_step_grad_f32 needs.
  * g2k_step_grad_f32: grad [P + 2] = {d loss / d params summed over the S
  *   scenes (P floats), loss, count of (frame, pedestrian) pairs}, fixed

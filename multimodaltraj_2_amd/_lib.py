@@ -28,11 +28,12 @@ class G2KDims(ctypes.Structure):
 
 STEP_PRED_PED_MAJOR = 1      # g2k_dims.flags (include/g2k_hip.h)
 STEP_TARGETS_SHARED = 2
+STEP_LOSS_NLL = 4
 
 
 class G2KWeights(ctypes.Structure):
     _fields_ = [("Wi", c_vp), ("Wii", c_vp), ("Wv", c_vp), ("bv", c_vp), ("Wr", c_vp),
-                ("Wc", c_vp), ("Wo", c_vp)]
+                ("Wc", c_vp), ("Wo", c_vp), ("head", c_vp)]
 
 
 SYMBOLS = {

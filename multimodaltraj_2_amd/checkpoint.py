@@ -288,6 +288,7 @@ REF_NAMES = {
     "Wo": ("krnl_weights", "weight_o"),
     "Wc": ("krnl_weights", "weight_c"),
     "Wr": ("krnl_embed", "weight_r"),
+    "head": ("nll_head", "head"),      # the build's NLL head (no reference counterpart)
 }
 
 
@@ -322,7 +323,7 @@ def save_params(prefix: str, params, scope_index: int = 0, extras: dict | None =
     krnl_weights/cost).  Returns the names written."""
     from dataclasses import fields
     t = {ref_name(f.name, scope_index): getattr(params, f.name).detach().cpu().numpy().astype(dtype)
-         for f in fields(params)}
+         for f in fields(params) if getattr(params, f.name) is not None}
     t.update(extras or {})
     names = write_bundle(prefix, t)
     write_state(os.path.dirname(os.path.abspath(prefix)), prefix)
@@ -359,6 +360,10 @@ def load_params(prefix: str, scope_index: int | None = None, nmax: int | None = 
     vals = {}
     for f in fields(G2KParams):
         name = ref_name(f.name, k)
+        if f.name == "head":                 # optional (NLL-trained checkpoints only)
+            if name in t:
+                vals["head"] = np.asarray(t[name], dtype=np.float32)
+            continue
         if name not in t:
             raise KeyError(f"{prefix}: {name} missing")
         vals[f.name] = np.asarray(t[name], dtype=np.float32)

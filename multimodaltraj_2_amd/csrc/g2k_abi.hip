@@ -68,8 +68,10 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // inputs of the fused step (reference and train mode)
 int validate_step_inputs(const g2k_dims* d, const g2k_weights* w, const float* pos,
                          const float* vislet, const float* G, const float* targets,
-                         const int32_t* n_active) {
-  int rc = validate_common(d, true, false, G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED);
+                         const int32_t* n_active, bool train = false) {
+  int rc = validate_common(d, true, false,
+                           G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED |
+                               (train ? G2K_STEP_LOSS_NLL : 0));
   if (rc) return rc;
   if ((rc = validate_weights(w, true))) return rc;
   if (d->stride < 0) return set_err(G2K_EINVAL, "stride=%d < 0", d->stride);
@@ -93,7 +95,7 @@ StepArgs step_args(const g2k_dims* d, const g2k_weights* w, const float* pos, co
 
 // [S][P + 2] gradient rows, then one 64-byte line for the update ticket
 int64_t grad_rows_bytes(const g2k_dims* d) {
-  return (int64_t)d->S * (grad_params(d->Nmax) + 2) * 4 + 64;
+  return (int64_t)d->S * (grad_params(d->Nmax, loss_nll(*d)) + 2) * 4 + 64;
 }
 
 // train mode after the inputs are validated: the fused step with gradient
@@ -101,8 +103,9 @@ int64_t grad_rows_bytes(const g2k_dims* d) {
 // `params` is given
 int train_launch(StepArgs a, float* grad, void* workspace, int64_t workspace_bytes, float* params,
                  float* ms, float lr, float decay, float grad_clip, hipStream_t st) {
-  const int width = grad_params(a.d.Nmax) + 2;
+  const int width = grad_params(a.d.Nmax, loss_nll(a.d)) + 2;
   if (!grad) return set_err(G2K_EINVAL, "grad is NULL");
+  if (loss_nll(a.d) && !a.w.head) return set_err(G2K_EINVAL, "G2K_STEP_LOSS_NLL needs weights->head");
   const int64_t need = grad_rows_bytes(&a.d);
   if (!workspace || workspace_bytes < need)
     return set_err(G2K_EINVAL, "workspace of %lld bytes needed (got %lld)", (long long)need,
@@ -138,6 +141,7 @@ int g2k_abi_version(void) { return G2K_ABI_VERSION; }
 const char* g2k_last_error(void) { return g_err; }
 
 constexpr int kStepFlags = G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED;
+constexpr int kTrainFlags = kStepFlags | G2K_STEP_LOSS_NLL;
 
 int64_t g2k_step_lds_bytes(const g2k_dims* d) {
   if (validate_common(d, true, false, kStepFlags) != G2K_OK) return 0;
@@ -172,7 +176,7 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
 }
 
 int64_t g2k_train_workspace_bytes(const g2k_dims* d) {
-  if (validate_common(d, true, false, kStepFlags) != G2K_OK) return -1;
+  if (validate_common(d, true, false, kTrainFlags) != G2K_OK) return -1;
   return grad_rows_bytes(d);
 }
 
@@ -183,7 +187,7 @@ int g2k_train_step_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
                        float* metrics, float lambda, float* grad, void* workspace,
                        int64_t workspace_bytes, float* params, float* ms, float lr, float decay,
                        float grad_clip, void* stream) {
-  int rc = validate_step_inputs(d, w, pos, vislet, G, targets, n_active);
+  int rc = validate_step_inputs(d, w, pos, vislet, G, targets, n_active, true);
   if (rc) return rc;
   if ((rc = validate_H(d->H))) return rc;
   if (!h_in || !h_out || !pred || !metrics)
@@ -276,12 +280,12 @@ int g2k_gridlstm_f32(const float* in, int64_t ld_in, const float* state, int64_t
 }
 
 int64_t g2k_grad_size(const g2k_dims* d) {
-  if (validate_common(d, false, false, kStepFlags) != G2K_OK) return -1;
-  return grad_params(d->Nmax);
+  if (validate_common(d, false, false, kTrainFlags) != G2K_OK) return -1;
+  return grad_params(d->Nmax, loss_nll(*d));
 }
 
 int64_t g2k_grad_workspace_bytes(const g2k_dims* d) {
-  if (validate_common(d, true, false, kStepFlags) != G2K_OK) return -1;
+  if (validate_common(d, true, false, kTrainFlags) != G2K_OK) return -1;
   return grad_rows_bytes(d);
 }
 
@@ -290,7 +294,7 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
                       const int32_t* n_active, const int32_t* n_frames, const uint8_t* ped_mask,
                       float lambda, float* grad, void* workspace, int64_t workspace_bytes,
                       void* stream) {
-  int rc = validate_step_inputs(d, w, pos, vislet, G, targets, n_active);
+  int rc = validate_step_inputs(d, w, pos, vislet, G, targets, n_active, true);
   if (rc) return rc;
   StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda);
   return train_launch(a, grad, workspace, workspace_bytes, nullptr, nullptr, 0.f, 0.f, 0.f,
@@ -304,7 +308,7 @@ int g2k_step_grad_update_f32(const g2k_dims* d, const g2k_weights* w, const floa
                              int64_t workspace_bytes, float* params, float* ms, float lr,
                              float decay, float grad_clip, void* stream) {
   if (!params) return set_err(G2K_EINVAL, "params is NULL");
-  int rc = validate_step_inputs(d, w, pos, vislet, G, targets, n_active);
+  int rc = validate_step_inputs(d, w, pos, vislet, G, targets, n_active, true);
   if (rc) return rc;
   StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda);
   return train_launch(a, grad, workspace, workspace_bytes, params, ms, lr, decay, grad_clip,

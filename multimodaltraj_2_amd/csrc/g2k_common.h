@@ -409,7 +409,12 @@ struct StepArgs {
 int scene_step_launch(const StepArgs& a, hipStream_t st);
 int64_t scene_lds_bytes(const g2k_dims* d, bool grad);
 
-__host__ __device__ inline int grad_params(int Nmax) { return 24 * Nmax + 496; }
+// floats of one parameter vector (g2k_grad_size): + the NLL head [3][12]
+constexpr int kNllHead = 3 * kL;
+__host__ __device__ inline int grad_params(int Nmax, bool nll = false) {
+  return 24 * Nmax + 496 + (nll ? kNllHead : 0);
+}
+__host__ __device__ inline bool loss_nll(const g2k_dims& d) { return (d.flags & G2K_STEP_LOSS_NLL) != 0; }
 
 // g2k_train.hip
 // the optimizer step folded into the gradient-row sum (run by the workgroup

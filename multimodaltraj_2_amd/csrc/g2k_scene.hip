@@ -63,13 +63,19 @@ struct SceneLayout {
   int wtot;            // window rows of the whole scene ((F - 1) * stride + T)
   int dwo_seq;         // 1: dWo^T accumulated in frame order (one copy); 0: one copy per producer
   int o_cost, o_gframe, o_gpriv, o_gpdv, o_gacc, o_gdv, o_gdwo, o_gseq;
+  // train mode with the NLL loss (zero-sized otherwise): per-lane head-gradient
+  // sums [NG][64][12], per-worker sums [NG][36], the head's raw values [36] and
+  // its per-step constants [5][12] (1/sigma_x, 1/sigma_y, rho, 1/(1-rho^2), base)
+  int o_nlla, o_nllw, o_nllr, o_nllc;
+  int tfb;             // target bytes per frame (0: one set for every frame, G2K_STEP_TARGETS_SHARED)
   int total;           // floats
 };
 
 __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int F, int fc, int NP,
-                                                       bool grad) {
+                                                       bool grad, bool nll = false) {
   SceneLayout s;
   s.fc = fc;
+  s.tfb = Nmax * kL2 * 4;
   s.wcmax = (fc - 1) * stride + kT;
   s.pp = 2 * Nmax;                            // unpadded: the chunk's rows are one contiguous copy
   int o = 0;
@@ -91,6 +97,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.wtot = (F > 0 ? F - 1 : 0) * stride + kT;
   s.dwo_seq = (int64_t)(NP + kRecW) * Nmax * kT * 4 > 32 * 1024 ? 1 : 0;
   s.o_cost = s.o_gframe = s.o_gpriv = s.o_gpdv = s.o_gacc = s.o_gdv = s.o_gdwo = s.o_gseq = o;
+  s.o_nlla = s.o_nllw = s.o_nllr = s.o_nllc = o;
   if (grad) {
     s.o_cost = o;   o += fc * kT * kT;                 // cost_f per chunk frame (head -> terms)
     s.o_gframe = o; o += NG * kGFrame;
@@ -99,19 +106,25 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
     s.o_gpdv = o;   o += NG * s.wcmax * kD;            // ... and of its dU rows in the chunk
     s.o_gdv = o;    o += rup4(s.wtot * kD);            // dV: window-row gradient [wtot][16]
     s.o_gdwo = o;   o += (s.dwo_seq ? 1 : NG) * Nmax * kT;   // dWo^T [Nmax][8]
+    s.o_nlla = o;   o += nll ? NG * 64 * 12 : 0;       // (zeroed with the sums above)
+    s.o_nllw = o;   o += nll ? NG * kNllHead : 0;
     s.o_gseq = o;   o += rup4(2 + (Nmax + 15) / 16);   // chunk count, -, dWo tile seqs
+    s.o_nllr = o;   o += nll ? kNllHead : 0;
+    s.o_nllc = o;   o += nll ? 5 * kL : 0;
   }
   s.total = o;
   return s;
 }
 
 __host__ inline SceneLayout scene_layout(const g2k_dims* d, int NP, bool grad) {
+  const bool nll = grad && loss_nll(*d);
   int fc = d->F < 1 ? 1 : (d->F < kSceneChunk ? d->F : kSceneChunk);
-  SceneLayout l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad);
+  SceneLayout l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad, nll);
   while ((int64_t)l.total * 4 > 160 * 1024 && fc > 1) {
     fc = (fc + 1) / 2;
-    l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad);
+    l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad, nll);
   }
+  l.tfb = (d->flags & G2K_STEP_TARGETS_SHARED) ? 0 : d->Nmax * kL2 * 4;
   return l;
 }
 
@@ -305,7 +318,7 @@ struct SceneCtx {
   int* sGseq;     // train: [0] producers done with the chunk's frames (cumulative), [2 + t]
                   // frames added to dWo tile t (dwo_seq)
   int s, tid, lane, wv, L, q, nact, nf, ntiles, ntact;
-  int tfs;        // 1: targets per frame; 0: one set for all frames (G2K_STEP_TARGETS_SHARED)
+  float *sNllA, *sNllW, *sNllR, *sNllC;   // NLL loss (see SceneLayout)
 };
 
 // LDS-DMA of a chunk's position window rows (train.py:76-79 window) into
@@ -456,12 +469,28 @@ __device__ __forceinline__ void scene_kmats(const SceneCtx& c) {
   }
 }
 
+// NLL loss: the head's per-step constants from its raw values (one lane per
+// step): 1/sigma_x, 1/sigma_y, rho, 1/(1 - rho^2), log(2 pi) + log sigma_x +
+// log sigma_y + 1/2 log(1 - rho^2), as g2k_nll_kernel forms them.
+__device__ __forceinline__ void scene_nll_consts(const SceneCtx& c) {
+  const int t = c.lane;
+  if (t < kL) {
+    const float lsx = c.sNllR[t], lsy = c.sNllR[kL + t], r = c.sNllR[2 * kL + t];
+    const float rho = tanhf(r), cc = 1.f - rho * rho;
+    c.sNllC[t] = expf(-lsx);
+    c.sNllC[kL + t] = expf(-lsy);
+    c.sNllC[2 * kL + t] = rho;
+    c.sNllC[3 * kL + t] = 1.f / cc;
+    c.sNllC[4 * kL + t] = 1.8378770664093453f + lsx + lsy + 0.5f * logf(cc);
+  }
+}
+
 // Chunk staging shared by both roles (every wave takes part).  The chunk's
 // position window is in flight by LDS-DMA.  Wait, barrier; the producer
 // waves compute the embedding-row tiles (scene_vtile) and, at the first
 // chunk, K1 / K2 (scene_kmats) while `rec_init` runs on the recurrence
 // waves (softmax(h) numerators); barrier.
-template <int NT, int NP, int VMC, typename RecInit>
+template <int NT, int NP, int VMC, bool NLL = false, typename RecInit>
 __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int fb, int cnt, bool hl,
                                             RecInit rec_init) {
@@ -475,8 +504,12 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
     const int ntile = (wcc + 3 + 15) / 16;
     const int ntask = ntile + (fb == 0 ? 1 : 0);
     for (int task = c.wv - kRecW; task < ntask; task += NP) {
-      if (task < ntile) scene_vtile(a, lay, c, 16 * task, wcc);
-      else scene_kmats(c);
+      if (task < ntile) {
+        scene_vtile(a, lay, c, 16 * task, wcc);
+      } else {
+        scene_kmats(c);
+        if (NLL) scene_nll_consts(c);
+      }
     }
   } else {
     rec_init();
@@ -579,11 +612,45 @@ __device__ __forceinline__ int mrow(int r) { return (r & 1) * kL + (r >> 1); }
 // `after_targets` runs once the target registers are consumed (GRAD: the
 // next tile's targets are loaded into them there, before this tile's stores,
 // so the next tile's wait counts exactly those stores).
-template <bool GRAD, bool PM, typename AfterTargets>
+// NLL (train mode): the loss of this lane's four (x, y) pairs — steps 2q, 2q+1
+// (d0) and 8+2q, 9+2q (d1, q < 2) — around pred with the head's per-step
+// constants (sC [5][12]); d0 / d1 (= Y - target) are replaced by d nll / d Y,
+// the nll is added to lsum and the head's gradient terms (d/dlog sigma_x,
+// d/dlog sigma_y, d/datanh rho of pair j) into the lane's LDS sums sA[(3 j + k)
+// * 64] (lane-minor: conflict-free).  One pair at a time, its constants and
+// sums loaded right before use (few live registers: the caller is at the
+// VGPR limit).
+__device__ __forceinline__ void nll_pairs(const float* sC, float* sA, int q, bool has_t,
+                                          float (&d0)[4], float (&d1)[4], float& lsum) {
+  const bool hi = q < 2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    asm volatile("" ::: "memory");                           // keep each pair's loads here
+    const bool blk1 = j >= 2;
+    const int st = blk1 ? (hi ? 8 + 2 * q + (j & 1) : 8) : 2 * q + (j & 1);
+    const float w = (has_t && (!blk1 || hi)) ? 1.f : 0.f;
+    float* d = blk1 ? d1 : d0;
+    const float isx = sC[st], isy = sC[kL + st], rho = sC[2 * kL + st], ic = sC[3 * kL + st],
+                base = sC[4 * kL + st];
+    float* g = sA + 3 * j * 64;
+    const float g0 = g[0], g1 = g[64], g2 = g[128];
+    const float a = -d[2 * (j & 1)] * isx, b = -d[2 * (j & 1) + 1] * isy;   // (target - mu) / sigma
+    const float ab = a * b, z = fmaf(a, a, fmaf(b, b, -2.f * rho * ab));
+    lsum = fmaf(w, fmaf(0.5f * ic, z, base), lsum);
+    d[2 * (j & 1)] = w * (-(a - rho * b) * ic * isx);
+    d[2 * (j & 1) + 1] = w * (-(b - rho * a) * ic * isy);
+    g[0] = fmaf(w, 1.f - (a * a - rho * ab) * ic, g0);
+    g[64] = fmaf(w, 1.f - (b * b - rho * ab) * ic, g1);
+    g[128] = fmaf(w, -rho - ab + rho * z * ic, g2);
+  }
+}
+
+template <bool GRAD, bool PM, bool NLL, typename AfterTargets>
 __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, brsrc pr,
                                           const float2 (&tg)[4], bool has_t, int Nmax, int nact,
                                           int t, int L, int q, float acc[5], float& lsum,
-                                          f32x4 (&dm)[2], f32x4& dWoT, AfterTargets after_targets) {
+                                          f32x4 (&dm)[2], f32x4& dWoT, AfterTargets after_targets,
+                                          const float* nllC = nullptr, float* nllA = nullptr) {
   const int n0 = 16 * t, n = n0 + L;
   const bool hi = q < 2;                                   // block-1 rows exist (r < 24)
   f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
@@ -638,9 +705,10 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
       bstore(pr, (n < Nmax && hi) ? (mrow(16 + 4 * q + v) * Nmax + n) * 4 : kBufOff, y1[v]);
     }
   }
-  if (GRAD) {
+  if (GRAD && !NLL) {
     // M's operand of dWo^T, loaded here (not with Y's operands) so that it is
     // not live across the stores; its latency hides under the error terms
+    // (NLL: after the loss terms, which need the registers first)
     const int L7 = L & 7;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -694,9 +762,18 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
     acc[1] += g1;
     acc[2] = fmaf(g1, fsq, acc[2]);
     acc[4] = fmaf(g1, __builtin_amdgcn_sqrtf(fsq), acc[4]);
-    if (GRAD) lsum = fmaf(g1, sa + sc, lsum);
+    if (GRAD && !NLL) lsum = fmaf(g1, sa + sc, lsum);
   }
   if (GRAD) {
+    if (NLL) {
+      nll_pairs(nllC, nllA, q, has_t, d0, d1, lsum);         // dY = d nll / d Y (masked)
+      const int L7 = L & 7;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bm[ks] = M[mrow(4 * q + ks) * kT + L7];
+        bm[4 + ks] = M[mrow(16 + 4 * (q & 1) + ks) * kT + L7];
+      }
+    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       d0[v] = has_t ? d0[v] : 0.f;
@@ -966,12 +1043,15 @@ __device__ __forceinline__ int grad_rec_frames(int cnt, int NP) { return cnt >= 
 // 16 t + L, floats 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row, zero
 // for q >= 2) by range-checked buffer loads (no branch: !ok and inactive
 // pedestrians n >= n_active read zeros without touching memory).
-// tfs = 0: one target set for every frame (G2K_STEP_TARGETS_SHARED).
+// tfb = SceneLayout::tfb, the bytes between two frames' targets (0: one set
+// for every frame, G2K_STEP_TARGETS_SHARED) — a kernel argument, so the
+// option costs the train-mode producers no register (a per-call select of
+// the flag spilled one there).
 __device__ __forceinline__ void load_targets(brsrc tgr, int Nmax, int nact, int fb, int fl, int t,
-                                             bool ok, int L, int q, float2 (&tg)[4], int tfs) {
+                                             bool ok, int L, int q, float2 (&tg)[4], int tfb) {
   const int ne = 16 * t + L;
   ok = ok && ne < nact;
-  const int base = ((((fb + fl) & -tfs) * Nmax + (ne < Nmax ? ne : 0)) * kL2) * 4;
+  const int base = (fb + fl) * tfb + (ne < Nmax ? ne : 0) * (kL2 * 4);
   // two 16-B loads (rows are 96 B: every float4 is 16-B aligned)
   const float4 u = bload4(tgr, ok ? base + 16 * q : kBufOff);
   const float4 w = bload4(tgr, ok && q < 2 ? base + 64 + 16 * q : kBufOff);
@@ -1009,7 +1089,7 @@ __device__ __forceinline__ void balance_stores(const StepArgs& a) {
 // each tile loads the next tile's targets as soon as its own are consumed,
 // before its prediction stores (tg holds the first tile's targets on entry
 // when `preloaded`).
-template <bool PM>
+template <bool PM, bool NLL>
 __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int slot, int fb, int f0, int fstep,
                                             int fend, unsigned act_bits, float (&acc)[5],
@@ -1017,7 +1097,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
   const int Nmax = a.d.Nmax, F = a.d.F, L = c.L, q = c.q, ntact = c.ntact;
   const brsrc tgr = scene_targets_rsrc(a, c.s);
   if (!preloaded) {
-    load_targets(tgr, Nmax, c.nact, fb, f0, 0, f0 < fend, L, q, tg, c.tfs);
+    load_targets(tgr, Nmax, c.nact, fb, f0, 0, f0 < fend, L, q, tg, lay.tfb);
     balance_stores<PM>(a);
   }
   float* ys = c.sY + slot * kL2 * kYP;
@@ -1031,9 +1111,10 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
       const bool nxt = t + 1 < ntact;                    // the next tile: this frame's, else the next frame's
       const int nfl = nxt ? fl : fl + fstep, nt = nxt ? t + 1 : 0;
       f32x4 dWoT;
-      pred_tile<true, PM>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u, Nmax,
-                          c.nact, t, L, q, acc, lsum, dm, dWoT,
-                          [&] { load_targets(tgr, Nmax, c.nact, fb, nfl, nt, nfl < fend, L, q, tg, c.tfs); });
+      pred_tile<true, PM, NLL>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u,
+                               Nmax, c.nact, t, L, q, acc, lsum, dm, dWoT,
+                               [&] { load_targets(tgr, Nmax, c.nact, fb, nfl, nt, nfl < fend, L, q, tg, lay.tfb); },
+                               c.sNllC, c.sNllA + slot * 12 * 64 + c.lane);
       // dWo^T[n0 + 4q + v][t = L]: one copy per worker, or one copy added
       // to in frame order (tile sequence word) when that is too big
       const int nb = 16 * t + 4 * q;
@@ -1061,6 +1142,23 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
     frame_grad(a, lay, c, fl, dm, slot);
     dm[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     dm[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// NLL: a worker's per-lane head-gradient sums reduced over the 16 lanes
+// (pedestrians) of each lane group into its row [36] (k * 12 + step): lane
+// group q holds steps 2q, 2q+1 (sums 0..5) and 8+2q, 9+2q (6..11, q < 2).
+__device__ __forceinline__ void nll_worker_reduce(const SceneCtx& c, int slot) {
+  const float* a = c.sNllA + slot * 12 * 64 + c.lane;
+  float* w = c.sNllW + slot * kNllHead;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int st = j < 2 ? 2 * c.q + j : 8 + 2 * c.q + (j - 2);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float v = row16_sum(a[(3 * j + k) * 64]);
+      if (c.L == 0 && (j < 2 || c.q < 2)) w[k * kL + st] = v;
+    }
   }
 }
 
@@ -1100,7 +1198,7 @@ __device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCt
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
-template <int NP, bool GRAD, bool PM>
+template <int NP, bool GRAD, bool PM, bool NLL>
 __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLayout& lay,
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
@@ -1123,14 +1221,14 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     const bool ok = k < nitems;
     int fl, t;
     item_ft(ok ? k : 0, fl, t);
-    load_targets(tgr, Nmax, c.nact, fb, fl, t, ok, L, q, tg, c.tfs);
+    load_targets(tgr, Nmax, c.nact, fb, fl, t, ok, L, q, tg, lay.tfb);
   };
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float lsum = 0.f;
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
-    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});
+    scene_stage<64 * (kRecW + NP), NP, 0, NLL>(a, lay, c, fb, cnt, false, [] {});
     const int nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;   // forward
     // GRAD: this producer's frames pw, pw + NP, ... < gend of the chunk (the
     // last R frames of the last chunk go to the recurrence waves)
@@ -1139,7 +1237,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // the first tiles' targets: in flight during the heads (GRAD: one buffer
     // and the balancing stores, see grad_frames)
     if (GRAD) {
-      load_targets(tgr, Nmax, c.nact, fb, pw, 0, pw < gend, L, q, tgA, c.tfs);
+      load_targets(tgr, Nmax, c.nact, fb, pw, 0, pw < gend, L, q, tgA, lay.tfb);
       balance_stores<PM>(a);
     } else {
       load_item(fb, nitems, 0, tgA);
@@ -1180,7 +1278,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     }
     // phase 2 — predictions and errors (GRAD: and the gradient)
     if (GRAD) {
-      grad_frames<PM>(a, lay, c, pw, fb, pw, NP, gend, act_bits, acc, lsum, tgA, true);
+      grad_frames<PM, NLL>(a, lay, c, pw, fb, pw, NP, gend, act_bits, acc, lsum, tgA, true);
       // every worker done with the chunk's frames -> its dU rows into dV
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) atomicAdd(c.sGseq, 1);
@@ -1196,8 +1294,9 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
         const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : a.targets,
                                     a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
         f32x4 dWoT;
-        pred_tile<false, PM>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tg, (act_bits >> t) & 1u,
-                             Nmax, c.nact, t, L, q, acc, lsum, dm, dWoT, [] {});
+        pred_tile<false, PM, false>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tg,
+                                    (act_bits >> t) & 1u, Nmax, c.nact, t, L, q, acc, lsum, dm,
+                                    dWoT, [] {});
       };
       for (int k = 0; k < nitems; k += 2) {
         item(k, tgA);
@@ -1211,6 +1310,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
   }
   // metrics (and the loss): GRAD also the recurrence waves' rows (NP + w)
+  if (NLL) nll_worker_reduce(c, pw);
   publish_metrics(a, c, pw, GRAD ? NP + kRecW : NP, acc, lsum, GRAD);
   if (!GRAD) return;
   // GRAD: every producer has added its frames once the ticket count is NP;
@@ -1221,12 +1321,13 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) atomicAdd(c.sGseq + 1, 1);
   poll_word(c.sGseq + 1, NP);
-  const int P = 24 * Nmax + 496;
+  const int P = grad_params(Nmax, NLL);
   float* row = a.grad_rows + (size_t)s * (P + 2);
   const float* ga = c.sGAcc;
   const float* sm = c.sm;
   const int o_wii = Nmax * kD, o_wv = o_wii + kD * kT, o_bv = o_wv + kT * (kD + 2),
-            o_wr = o_bv + kD, o_wc = o_wr + kT * 2, o_wo = o_wc + kL2 * kT;
+            o_wr = o_bv + kD, o_wc = o_wr + kT * 2, o_wo = o_wc + kL2 * kT,
+            o_head = o_wo + kT * Nmax;
   // dWi[n][d] = sum_w N[w][n] dV[w][d] + vislet[0][n] dVe[0][d] + vislet[1][n] dVe[1][d]
   // (train.py:76-85 norms of the whole window, re-read from the position rows)
   // by MFMA per 16-pedestrian tile: A[n = L][w] = N[w][n0 + L], B[w][d = L] = dV[w][d]
@@ -1296,16 +1397,18 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       x = 0.f;                                        // Wr does not reach the predictions
     } else if (p < o_wo) {
       x = ga[kGA_WC + p - o_wc];
-    } else if (p < P) {                               // dWo[t][n]
+    } else if (p < o_head) {                          // dWo[t][n]
       const int q2 = p - o_wo, t = q2 / Nmax, nn = q2 - t * Nmax;
       if (lay.dwo_seq) {
         x = c.sGdWo[nn * kT + t];
       } else {
         for (int pr = 0; pr < NP + kRecW; ++pr) x += c.sGdWo[(pr * Nmax + nn) * kT + t];
       }
-    } else if (p == P) {                              // loss = 1/2 sum dY^2, worker order
+    } else if (p < P) {                               // NLL head gradient, worker order
+      for (int pr = 0; pr < NP + kRecW; ++pr) x += c.sNllW[pr * kNllHead + (p - o_head)];
+    } else if (p == P) {                              // loss: 1/2 sum dY^2 (NLL: sum nll), worker order
       for (int pr = 0; pr < NP + kRecW; ++pr) x += c.sMet[pr * 8 + 5];
-      x *= 0.5f;
+      x *= NLL ? 1.f : 0.5f;
     } else {                                          // count of (frame, pedestrian) pairs
       for (int pr = 0; pr < NP + kRecW; ++pr) x += c.sMet[pr * 8 + 1];
     }
@@ -1316,7 +1419,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
 // GRAD, recurrence wave w after its recurrence: the last R frames of the
 // last chunk (frame cnt - R + w) as gradient worker NP + w, then its metrics
 // row and ticket (with zero partials when R = 0).
-template <int NP, bool PM>
+template <int NP, bool PM, bool NLL>
 __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayout& lay,
                                               const SceneCtx& c) {
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1327,16 +1430,17 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
     const int R = grad_rec_frames(cnt, NP);
     if (R > 0) {
       float2 tg[4];
-      grad_frames<PM>(a, lay, c, NP + c.wv, fb, cnt - R + c.wv, R, cnt, scene_act_bits(a, c), acc,
-                      lsum, tg, false);
+      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, cnt - R + c.wv, R, cnt, scene_act_bits(a, c),
+                           acc, lsum, tg, false);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (c.lane == 0) atomicAdd(c.sGseq, 1);
     }
   }
+  if (NLL) nll_worker_reduce(c, NP + c.wv);
   publish_metrics(a, c, NP + c.wv, NP + kRecW, acc, lsum, true);
 }
 
-template <int TPW, int NP, bool GRAD, bool PM>
+template <int TPW, int NP, bool GRAD, bool PM, bool NLL>
 __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   constexpr int NT = 64 * (kRecW + NP);
   constexpr int kRB = 16 * kRecW;
@@ -1365,6 +1469,8 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   c.sGAcc = smem + lay.o_gacc;
   c.sGdV = smem + lay.o_gdv; c.sGdWo = smem + lay.o_gdwo;
   c.sGseq = reinterpret_cast<int*>(smem + lay.o_gseq);
+  c.sNllA = smem + lay.o_nlla; c.sNllW = smem + lay.o_nllw;
+  c.sNllR = smem + lay.o_nllr; c.sNllC = smem + lay.o_nllc;
   if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket
   if (GRAD) {                                          // accumulators and their sequence words
     for (int i = c.tid; i < lay.o_gseq + rup4(2 + c.ntiles) - lay.o_gacc; i += NT) smem[lay.o_gacc + i] = 0.f;
@@ -1377,7 +1483,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
     // the small segments: one wave each (one pointer per wave keeps the
     // kernel-argument loads off a serial s_load / s_waitcnt chain)
-    for (int seg = wv; seg < 10; seg += NT / 64) {
+    for (int seg = wv; seg < (NLL ? 11 : 10); seg += NT / 64) {
       const float* src;
       float* dst;
       int n;
@@ -1391,7 +1497,8 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
         case 6: src = a.w.Wr; dst = c.sm + SM_WR; n = kT * 2; break;
         case 7: src = a.w.Wc; dst = c.sm + SM_WC; n = kL2 * kT; break;
         case 8: src = a.vislet + (size_t)c.s * 2 * Nmax; dst = c.sVis; n = Nmax; break;
-        default: src = a.vislet + (size_t)c.s * 2 * Nmax + Nmax; dst = c.sVis + Nmax; n = Nmax; break;
+        case 9: src = a.vislet + (size_t)c.s * 2 * Nmax + Nmax; dst = c.sVis + Nmax; n = Nmax; break;
+        default: src = a.w.head; dst = c.sNllR; n = kNllHead; break;   // NLL head [3][12]
       }
       // 16 bytes per lane when both ends allow it (every segment of the
       // usual layouts): 11 wave-instructions instead of 26 through the CU's
@@ -1418,13 +1525,12 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     c.nf = a.n_frames ? clampi(nf, 0, F) : F;
   }
   c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians
-  c.tfs = (a.d.flags & G2K_STEP_TARGETS_SHARED) ? 0 : 1;
   if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
   if (c.wv < kRecW) {
     scene_recurrence<TPW, NP>(a, lay, c);
-    if (GRAD) rec_grad_work<NP, PM>(a, lay, c);
+    if (GRAD) rec_grad_work<NP, PM, NLL>(a, lay, c);
   } else
-    scene_producer<NP, GRAD, PM>(a, lay, c);
+    scene_producer<NP, GRAD, PM, NLL>(a, lay, c);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
 }
 
@@ -1443,14 +1549,20 @@ int scene_producers(int H, int Nmax, bool grad) {
   return grad ? 8 : 12;
 }
 
+template <int TPW, int NP, bool GRAD, bool PM>
+void launch_kp(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
+  const dim3 grid(a.d.S), block(64 * (kRecW + NP));
+  const size_t lds = (size_t)l.total * 4;
+  if (GRAD && loss_nll(a.d))
+    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, GRAD>), grid, block, lds, st, a, l);
+  else
+    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false>), grid, block, lds, st, a, l);
+}
+
 template <int TPW, int NP, bool GRAD>
 void launch_k(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
-  if (a.d.flags & G2K_STEP_PRED_PED_MAJOR)
-    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, true>), dim3(a.d.S), dim3(64 * (kRecW + NP)),
-                       (size_t)l.total * 4, st, a, l);
-  else
-    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, false>), dim3(a.d.S), dim3(64 * (kRecW + NP)),
-                       (size_t)l.total * 4, st, a, l);
+  if (a.d.flags & G2K_STEP_PRED_PED_MAJOR) launch_kp<TPW, NP, GRAD, true>(a, l, st);
+  else launch_kp<TPW, NP, GRAD, false>(a, l, st);
 }
 
 template <bool GRAD>

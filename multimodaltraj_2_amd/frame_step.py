@@ -34,22 +34,27 @@ class G2KParams:
     Wr: torch.Tensor    # [T, 2]      models/g2k_lstm_mcr.py:72-76
     Wc: torch.Tensor    # [2L, T]     models/g2k_lstm_mcr.py:65-69
     Wo: torch.Tensor    # [T, Nmax]   models/g2k_lstm_mcr.py:61-64
+    head: torch.Tensor | None = None   # [3, L] NLL head (train mode, loss "nll"; the build's)
 
     @property
     def nmax(self) -> int:
         return int(self.Wi.shape[0])
 
     def to(self, device) -> "G2KParams":
-        return G2KParams(**{f.name: getattr(self, f.name).to(device) for f in fields(self)})
+        return G2KParams(**{f.name: (None if getattr(self, f.name) is None
+                                     else getattr(self, f.name).to(device)) for f in fields(self)})
 
     def numpy(self) -> dict:
-        return {f.name: getattr(self, f.name).detach().cpu().numpy() for f in fields(self)}
+        return {f.name: getattr(self, f.name).detach().cpu().numpy() for f in fields(self)
+                if getattr(self, f.name) is not None}
 
     def check(self, device):
         D, T, L2 = HIDDEN_LEN, OBS_LEN, 2 * PRED_LEN
         n = self.nmax
         want = dict(Wi=(n, D), Wii=(D, T), Wv=(T, D + 2), bv=(D,), Wr=(T, 2), Wc=(L2, T),
                     Wo=(T, n))
+        if self.head is not None:
+            want["head"] = (3, PRED_LEN)
         for k, shp in want.items():
             t = getattr(self, k)
             if tuple(t.shape) != shp:
@@ -57,7 +62,8 @@ class G2KParams:
             _check_dev(k, t, device, torch.float32)
 
     def abi(self) -> _lib.G2KWeights:
-        return _lib.G2KWeights(*(getattr(self, f.name).data_ptr() for f in fields(self)))
+        return _lib.G2KWeights(*(None if getattr(self, f.name) is None else
+                                 getattr(self, f.name).data_ptr() for f in fields(self)))
 
 
 def init_params(nmax: int, seed: int = 0, device="cpu") -> G2KParams:
@@ -92,14 +98,18 @@ def _stream(stream):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-def step_flags(pred_layout="band", targets_shared=False) -> int:
+def step_flags(pred_layout="band", targets_shared=False, loss="l2") -> int:
     """g2k_dims.flags: pred_layout "band" = pred_path_band [S, F, 2L, Nmax],
     "ped" = pedestrian-major [S, F, Nmax, L, 2]; targets_shared = one
-    [S, 1, Nmax, L, 2] target set for every frame."""
+    [S, 1, Nmax, L, 2] target set for every frame; loss (train mode) "l2" =
+    1/2 the squared error, "nll" = the bivariate-Gaussian NLL (params.head)."""
     if pred_layout not in ("band", "ped"):
         raise ValueError(f"pred_layout {pred_layout!r}: 'band' or 'ped'")
+    if loss not in ("l2", "nll"):
+        raise ValueError(f"loss {loss!r}: 'l2' or 'nll'")
     return ((_lib.STEP_PRED_PED_MAJOR if pred_layout == "ped" else 0)
-            | (_lib.STEP_TARGETS_SHARED if targets_shared else 0))
+            | (_lib.STEP_TARGETS_SHARED if targets_shared else 0)
+            | (_lib.STEP_LOSS_NLL if loss == "nll" else 0))
 
 
 def pred_shape(S, F, Nmax, pred_layout="band"):

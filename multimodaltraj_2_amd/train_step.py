@@ -27,24 +27,33 @@ from .frame_step import (HIDDEN_LEN, LAMBDA, OBS_LEN, PRED_LEN, G2KParams, StepP
                          _ptr, _stream, step_flags, step_frames)
 
 GRAD_ORDER = ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo")   # g2k_weights order
+NLL_HEAD = 3 * PRED_LEN          # loss "nll": the head [3, L] follows Wo in the flat vector
 LEARNING_RATE = 0.005    # argParser.py:43
 DECAY_RATE = 0.95        # argParser.py:46 (RMSProp)
 GRAD_CLIP = 10.0         # argParser.py:40
 
 
-def grad_size(nmax: int) -> int:
-    """Floats in one parameter vector (g2k_grad_size): 24 * Nmax + 496."""
-    return 24 * int(nmax) + 496
+def grad_size(nmax: int, loss: str = "l2") -> int:
+    """Floats in one parameter vector (g2k_grad_size): 24 * Nmax + 496
+    (+ 36 for the NLL head)."""
+    return 24 * int(nmax) + 496 + (NLL_HEAD if loss == "nll" else 0)
 
 
-def flat_params(params: G2KParams):
+def flat_params(params: G2KParams, loss: str = "l2"):
     """Copy ``params`` into one flat device buffer in gradient layout and
     return (flat, G2KParams of views into it), so one update kernel and one
-    all-reduce cover every parameter."""
-    flat = torch.cat([getattr(params, k).reshape(-1) for k in GRAD_ORDER]).contiguous()
-    views, o = {}, 0
-    for k in GRAD_ORDER:
+    all-reduce cover every parameter.  loss "nll": the head follows Wo
+    (zeros — sigma = 1, rho = 0 — when params has none)."""
+    keys = GRAD_ORDER + (("head",) if loss == "nll" else ())
+    parts = []
+    for k in keys:
         t = getattr(params, k)
+        if t is None:
+            t = torch.zeros((3, PRED_LEN), device=params.Wo.device, dtype=torch.float32)
+        parts.append(t)
+    flat = torch.cat([t.reshape(-1) for t in parts]).contiguous()
+    views, o = {}, 0
+    for k, t in zip(keys, parts):
         views[k] = flat[o:o + t.numel()].view(t.shape)
         o += t.numel()
     return flat, G2KParams(**views)
@@ -56,7 +65,7 @@ class GradPlan:
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, *, n_frames=None,
                  ped_mask=None, stride=1, lam=LAMBDA, grad=None, stream=None,
-                 targets_shared=False, frames=None):
+                 targets_shared=False, frames=None, loss="l2"):
         lib = _lib.load()
         dev = pos.device
         if dev.type != "cuda":
@@ -79,8 +88,10 @@ class GradPlan:
             _check_dev("n_frames", n_frames, dev, torch.int32)
         if ped_mask is not None:
             _check_dev("ped_mask", ped_mask, dev, torch.uint8)
+        if loss == "nll" and params.head is None:
+            raise ValueError('loss "nll" needs params.head [3, 12]')
         d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 64, Nmax, W, stride,
-                         step_flags("band", targets_shared))
+                         step_flags("band", targets_shared, loss))
         P = int(lib.g2k_grad_size(ctypes.byref(d)))
         nws = int(lib.g2k_grad_workspace_bytes(ctypes.byref(d)))
         if P < 0 or nws < 0:
@@ -143,8 +154,10 @@ class TrainPlan:
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
                  ped_mask=None, stride=1, lam=LAMBDA, out=None, grad=None, stream=None,
-                 pred_layout="band", targets_shared=False, frames=None):
+                 pred_layout="band", targets_shared=False, frames=None, loss="l2"):
         lib = _lib.load()
+        if loss == "nll" and params.head is None:
+            raise ValueError('loss "nll" needs params.head [3, 12]')
         self.fwd = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
                             ped_mask=ped_mask, stride=stride, lam=lam, out=out, stream=stream,
                             pred_layout=pred_layout, targets_shared=targets_shared, frames=frames)
@@ -152,7 +165,7 @@ class TrainPlan:
         S, W, Nmax, _ = pos.shape
         F, H = step_frames(targets, targets_shared, frames), int(h.shape[2])
         d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride,
-                         step_flags(pred_layout, targets_shared))
+                         step_flags(pred_layout, targets_shared, loss))
         self.P = int(lib.g2k_grad_size(ctypes.byref(d)))
         nws = int(lib.g2k_train_workspace_bytes(ctypes.byref(d)))
         if self.P < 0 or nws < 0:
@@ -203,9 +216,10 @@ class TrainStep:
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
                  lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,
                  n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None,
-                 pred_layout="band", targets_shared=False, frames=None):
-        self._layout = dict(pred_layout=pred_layout, targets_shared=targets_shared, frames=frames)
-        self.flat, self.params = flat_params(params)
+                 pred_layout="band", targets_shared=False, frames=None, loss="l2"):
+        self._layout = dict(pred_layout=pred_layout, targets_shared=targets_shared, frames=frames,
+                            loss=loss)
+        self.flat, self.params = flat_params(params, loss)
         self.P = self.flat.numel()
         self.ms = torch.ones_like(self.flat) if rmsprop else None
         self.lr, self.decay, self.grad_clip = lr, decay, grad_clip
