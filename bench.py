@@ -295,6 +295,8 @@ def main(argv=None):
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="processes of the all-core CPU aggregate (0: the CPUs this job may use)")
     ap.add_argument("--no-train", action="store_true", help="skip the train-mode timing")
+    ap.add_argument("--loss", choices=("l2", "nll"), default="l2",
+                    help="train-mode loss: 1/2 squared error or the bivariate-Gaussian NLL")
     ap.add_argument("--pred-layout", choices=("ped", "band"), default="ped",
                     help="pred as [S, F, Nmax, L, 2] (the per-pedestrian view train.py:254 "
                          "transposes to; only active pedestrians written) or pred_path_band "
@@ -438,9 +440,11 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
     Timed like the reference-mode step over the same rotated batches."""
     from multimodaltraj_2_amd.train_step import TrainStep
     t0 = batches[0]
+    if args.loss == "nll":
+        params.head = torch.zeros((3, 12), device=dev)
     ts = TrainStep(params, t0["pos"], t0["vislet"], t0["G"], t0["targets"], t0["n_active"],
                    t0["h0"], n_frames=t0["n_frames"], ped_mask=t0["ped_mask"], stride=b.stride,
-                   **layout)
+                   loss=args.loss, **layout)
     for t in batches[1:]:
         ts.bind(t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
                 n_frames=t["n_frames"], ped_mask=t["ped_mask"])
@@ -454,8 +458,9 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
     kern_s = event_time(step, max(20, min(args.steps, 200)), torch.cuda.current_stream())
     abytes = train_algorithmic_bytes(b, H, pbytes, ts.P, layout["targets_shared"])
     achieved = abytes / kern_s / 1e9
-    return {"metric": "frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + L2 loss gradient + "
-                      "gradient all-reduce + RMSProp update",
+    return {"metric": f"frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + "
+                      f"{'L2' if args.loss == 'l2' else 'bivariate-Gaussian NLL'} loss gradient + "
+                      "gradient all-reduce + RMSProp update", "loss": args.loss,
             "value": b.frames * world * args.steps / el, "unit": "frames/s",
             "ms_per_step": el / args.steps * 1e3, "allreduce_bytes": int((ts.P + 2) * 4),
             "loss_per_prediction_last_step": float(gl[-2] / max(gl[-1], 1.0)),

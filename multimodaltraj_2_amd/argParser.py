@@ -42,6 +42,9 @@ class ArgsParser:
                              'rounded up to 16; larger scenes are left out)')
     parser.add_argument('--train_batch', type=int, default=256,
                         help='--mode train: scenes per global step (a multiple of the ranks)')
+    parser.add_argument('--loss', choices=('l2', 'nll'), default='l2',
+                        help='--mode train: 1/2 squared error of the predictions, or the '
+                             'bivariate-Gaussian NLL with a learned per-step head')
     parser.add_argument('--train_scenes', type=int, default=0,
                         help='--mode train: distinct scenes used (0: all of the fold)')
     parser.add_argument('--valid_from_seed', type=int, default=0,

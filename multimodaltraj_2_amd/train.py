@@ -32,7 +32,8 @@
 
 --mode train (the build's; the reference has no loss or optimizer): RMSProp
   (--learning_rate, --decay_rate, --grad_clip; argParser.py:38-47) on the L2
-  loss of the predictions over the fold's real scenes (realdata.plan_scenes:
+  loss of the predictions or (--loss nll) the bivariate-Gaussian NLL with a
+  learned per-step head, over the fold's real scenes (realdata.plan_scenes:
   sample.py's scene per frame pointer, every distinct window of the training
   datasets), --train_batch scenes per global step, each rank taking its
   contiguous shard (dist.shard_scenes) and ONE all-reduce of the flat gradient
@@ -238,14 +239,15 @@ class HipStepper:
         per = S // steps
         G = torch.from_numpy(context_G(args.seed, S)).to(device)
         h0 = torch.zeros((S, fs.HIDDEN_LEN, args.rnn_size), device=device)
-        self.flat, p = flat_params(fs.init_params(plan.Nmax, seed=args.seed, device=device))
+        loss = getattr(args, "loss", "l2")
+        self.flat, p = flat_params(fs.init_params(plan.Nmax, seed=args.seed, device=device), loss)
         self.ms = torch.ones_like(self.flat)          # TF RMSProp's "rms" slot starts at 1
         self.kw = dict(lr=args.learning_rate, decay=args.decay_rate, grad_clip=args.grad_clip)
         sl = lambda k, x: x[k * per:(k + 1) * per]                    # noqa: E731
         self.plans = [TrainPlan(p, sl(k, t["pos"]), sl(k, t["vislet"]), sl(k, G),
                                 sl(k, t["targets"]), sl(k, t["n_active"]), sl(k, h0),
                                 n_frames=sl(k, t["n_frames"]), ped_mask=sl(k, t["ped_mask"]),
-                                stride=0, lam=args.lambda_param) for k in range(steps)]
+                                stride=0, lam=args.lambda_param, loss=loss) for k in range(steps)]
         self._keep = (t, G, h0, p)
 
     def fused(self, k):
@@ -352,9 +354,11 @@ def run_train_mode(args, device, log=print):
     if rank == 0 and args.save_dir:
         flat = torch.from_numpy(params.astype(np.float32))
         from .train_step import GRAD_ORDER
+        keys = GRAD_ORDER + (("head",) if args.loss == "nll" else ())
         shapes = {k: tuple(getattr(fs.init_params(plan.Nmax), k).shape) for k in GRAD_ORDER}
+        shapes["head"] = (3, fs.PRED_LEN)
         views, o = {}, 0
-        for k in GRAD_ORDER:
+        for k in keys:
             n = int(np.prod(shapes[k]))
             views[k] = flat[o:o + n].view(shapes[k])
             o += n
