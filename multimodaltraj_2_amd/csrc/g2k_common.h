@@ -253,9 +253,10 @@ __device__ __forceinline__ void lds_store_flag(int* p, int v) {
 //    publish, while the other waves are still finishing theirs.
 //  - poll_red: spin on ONE wave's sequence word (lane L reads wave L & 3's:
 //    seq[w] = frames whose partials w has published, +1) together with that
-//    wave's row-partial quad of rows 4q..4q+3; the four waves' quads are then
-//    summed across each lane quad by DPP.  Data is stored before the word and
-//    read after it, so a current word means current data.
+//    wave's row-partial quad of rows 4q..4q+3 (raw: the four waves' quads
+//    are summed across each lane quad by DPP where Recur::body needs them).
+//    Data is stored before the word and read after it, so a current word
+//    means current data.
 // Busy poll for the first rounds, then s_sleep.
 __device__ __forceinline__ int read_as(const int* flag, const float* asrc, float4& b) {
   const uint32_t fa = lds_addr(flag), da = lds_addr(asrc);
@@ -281,10 +282,9 @@ __device__ __forceinline__ void wait_as(const int* flag, int want, const float* 
 }
 
 __device__ __forceinline__ void poll_red(const int* seq_w, int want_seq, const float* rslot,
-                                         float4& z) {
+                                         f32x4& r) {
   const uint32_t sa = lds_addr(seq_w), ra = lds_addr(rslot);
   int sq;
-  f32x4 r;
   for (int it = 0; it < kPollMax; ++it) {
     asm volatile(
         "ds_read_b32 %0, %2\n\t"
@@ -296,15 +296,6 @@ __device__ __forceinline__ void poll_red(const int* seq_w, int want_seq, const f
     if (__builtin_amdgcn_ballot_w64(sq < want_seq) == 0) break;
     if (it >= 8) __builtin_amdgcn_s_sleep(1);
   }
-  float zz[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float t = r[i];
-    t += dpp<0xB1>(t);   // quad_perm [1,0,3,2]
-    t += dpp<0x4E>(t);   // quad_perm [2,3,0,1]
-    zz[i] = t;
-  }
-  z = make_float4(zz[0], zz[1], zz[2], zz[3]);
 }
 
 // Wait until all four recurrence waves' sequence words reach `want`.

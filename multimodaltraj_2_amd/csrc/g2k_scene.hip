@@ -58,7 +58,7 @@ constexpr int kGA_WC = 0, kGA_K1 = 192, kGA_VE = 272, kGA_BV = 304;
 struct SceneLayout {
   int fc, wcmax, pp;   // frames per chunk, window rows per chunk, pos row pitch (floats)
   int o_wi, o_wo, o_vis, o_v, o_small, o_y, o_met, o_ring, o_mring, o_flag, o_mflag, o_red,
-      o_pos, o_vg;
+      o_pos, o_vg, o_mask;
   // train mode (zero-sized otherwise)
   int wtot;            // window rows of the whole scene ((F - 1) * stride + T)
   int dwo_seq;         // 1: dWo^T accumulated in frame order (one copy); 0: one copy per producer
@@ -82,6 +82,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_wi = o;    o += rup4(Nmax * kD);
   s.o_wo = o;    o += rup4(kT * Nmax);
   s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
+  s.o_mask = o;  o += rup4((Nmax + 3) / 4);            // the scene's ped_mask row (LDS-DMA, dword rows)
   s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
   s.o_small = o; o += kSceneSmall;
   const int NG = NP + kRecW;                          // train: producers + recurrence waves
@@ -489,17 +490,20 @@ __device__ __forceinline__ void scene_nll_consts(const SceneCtx& c) {
 // position window is in flight by LDS-DMA.  Wait, barrier; the producer
 // waves compute the embedding-row tiles (scene_vtile) and, at the first
 // chunk, K1 / K2 (scene_kmats) while `rec_init` runs on the recurrence
-// waves (softmax(h) numerators); barrier.
-template <int NT, int NP, int VMC, bool NLL = false, typename RecInit>
+// waves; barrier.  Both barriers are raw s_barriers after the waits they
+// need (__syncthreads() would also drain every load in flight).  The DMA
+// wait is the s_waitcnt BUILTIN, not inline asm: the compiler's wait
+// insertion then knows the LDS-DMA has landed.  (It cannot see a wait in
+// inline asm; believing the DMA of a later chunk still in flight, it put a
+// vmcnt(0) before the first LDS read after the staging — which drained the
+// first tiles' target loads, issued to fly under the frame heads, and held
+// the first head back by a full HBM round trip.)
+template <int NT, int NP, bool NLL = false, typename RecInit>
 __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout& lay,
-                                            const SceneCtx& c, int fb, int cnt, bool hl,
-                                            RecInit rec_init) {
+                                            const SceneCtx& c, int fb, int cnt, RecInit rec_init) {
   const int wcc = (cnt - 1) * a.d.stride + kT;
-  // VMC = vector-memory ops this wave issued after the LDS-DMA that may stay
-  // in flight (the recurrence's h loads at the first chunk, when hl)
-  if (VMC > 0 && fb == 0 && hl) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();                                              // B1: window + weights landed
+  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed
   if (c.wv >= kRecW) {
     const int ntile = (wcc + 3 + 15) / 16;
     const int ntask = ntile + (fb == 0 ? 1 : 0);
@@ -514,11 +518,16 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
   } else {
     rec_init();
   }
-  __syncthreads();                                              // B2: V, VG, K1, K2
+  __builtin_amdgcn_s_waitcnt(0xc07f);                           // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2
 }
 
 // Role 1: the recurrence (waves 0..3).  Without h_in (gradient only) the
-// waves only take part in the chunk barriers.
+// waves only take part in the chunk barriers.  h is loaded during the first
+// staging (after B1: the prologue's HBM burst, which every wave's B1 waits
+// for, stays free of it) and its softmax numerators are formed after B2,
+// while the producers compute the first frame heads the chain waits for
+// anyway.
 template <int TPW, int NP>
 __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneLayout& lay,
                                                  const SceneCtx& c) {
@@ -526,27 +535,25 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   constexpr int kRB = 16 * kRecW;
   const int H = a.d.H;
   const bool live = a.h_in != nullptr;
-  Recur<TPW, kRecW> rc;
-  asm volatile("" ::: "memory");   // h loads after the prologue's LDS-DMA (counted vmcnt)
-  if (live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
-  asm volatile("" ::: "memory");
+  RecurH<TPW, kRecW> rc;
   int* seq = reinterpret_cast<int*>(c.sRed + 2 * kRB);   // 2 partial buffers, seq words, row max
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) scene_pos_dma<NT>(a, lay, c, fb, cnt);
-    scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, live, [&] {
-      // softmax(h) numerators (first chunk): row max exchange (seq 1), then
-      // e and its row partials into buffer 0 (seq 2), no workgroup barrier
-      if (fb == 0 && live) {
-        rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
-        asm volatile("" ::: "memory");
-        if (c.lane == 0) lds_store_flag(seq + c.wv, 1);
-        poll_seq(seq + (c.L & 3), 1);
-        rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
-        asm volatile("" ::: "memory");
-        if (c.lane == 0) lds_store_flag(seq + c.wv, 2);
-      }
+    scene_stage<NT, NP>(a, lay, c, fb, cnt, [&] {
+      if (fb == 0 && live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
     });
+    if (fb == 0 && live) {
+      // softmax(h) numerators: row max exchange (seq 1), then e and its row
+      // partials into buffer 0 (seq 2), no workgroup barrier
+      rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
+      asm volatile("" ::: "memory");
+      if (c.lane == 0) lds_store_flag(seq + c.wv, 1);
+      poll_seq(seq + (c.L & 3), 1);
+      rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
+      asm volatile("" ::: "memory");
+      if (c.lane == 0) lds_store_flag(seq + c.wv, 2);
+    }
     if (live) {
       __builtin_amdgcn_s_setprio(2);
       const float* as_lane = c.sRing + c.L * kD + 4 * c.q;   // this lane's As row quad, ring slot 0
@@ -556,13 +563,13 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
       // at the loop edge waits for every outstanding LDS op, the publish too).
       auto frame = [&](int fl, float4& b, int& flq, float4& bn, int& fln) {
         const int g = fb + fl;                 // global frame index
-        float4 z;
+        f32x4 z;
         poll_red(seq + (c.L & 3), g + 2, c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, z);
         if (__builtin_amdgcn_readfirstlane(flq) != g + 1)
           wait_as(c.sFlag + fl, g + 1, as_lane + fl * kD * kD, b);
         const int fn = fl + 1 < cnt ? fl + 1 : fl;   // next frame's ring slot (itself at the end)
         rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,
-                    as_lane + fn * kD * kD, fln, bn);
+                    as_lane + fn * kD * kD, fln, bn, g + 1 == c.nf);
       };
       float4 b0, b1;
       int f0 = read_as(c.sFlag, as_lane, b0), f1 = 0;
@@ -575,6 +582,7 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
   }
   if (!live) return;
+  if (c.nf == 0) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);   // h passes unchanged
   // epilogue straight off the last frame: wait for every wave's last
   // partials (its sequence word), h = adj * h', store; no workgroup barrier
   // (the producers finish the metrics on their own, scene_producer)
@@ -997,31 +1005,45 @@ __device__ __forceinline__ void grad_priv_sum(const SceneCtx& c, int NP) {
   }
 }
 
-// Pedestrian n = 16 t + L has targets (n < n_active and its ped_mask byte
-// set): bit t of the lane's word.  The mask row is read as one dword per lane
-// (pedestrians 4l .. 4l + 3 in lane l) and spread by four ballots: one
-// global round trip per wave, not one per 64 pedestrians (each was a
-// dependent byte load; a mask load inside the tile loop would also make the
-// compiler wait for the targets prefetched behind it).
-__device__ __forceinline__ unsigned scene_act_bits(const StepArgs& a, const SceneCtx& c) {
+// This lane's dword of the scene's ped_mask row (pedestrians 4 lane ..
+// 4 lane + 3; all ones without a mask).  A dword-aligned row arrived with the
+// prologue's LDS-DMA (segment 11): one LDS read.  (Loaded at the top of the
+// producer role, it was a dependent HBM miss behind the n_active scalar
+// load that every producer waited for before the staging barrier.)  Rows
+// that are not dword-aligned are read from global memory here.
+__device__ __forceinline__ bool mask_one_load(const StepArgs& a) {
+  return a.ped_mask && (a.d.Nmax & 3) == 0 && (((uintptr_t)a.ped_mask) & 3) == 0;
+}
+__device__ __forceinline__ uint32_t scene_mask_word(const StepArgs& a, const SceneLayout& lay,
+                                                    const SceneCtx& c) {
   const int Nmax = a.d.Nmax;
-  unsigned long long B[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // bit l: pedestrian 4 l + b has a target
-  if (a.ped_mask) {
-    const uint8_t* pm = a.ped_mask + (size_t)c.s * Nmax;
-    uint32_t w = 0;
-    if ((Nmax & 3) == 0 && (((uintptr_t)a.ped_mask) & 3) == 0) {
-      const int l = c.lane < Nmax / 4 ? c.lane : 0;
-      w = reinterpret_cast<const uint32_t*>(pm)[l];
-    } else {
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int n = 4 * c.lane + b;
-        w |= (uint32_t)(n < Nmax ? pm[n] : 0) << (8 * b);
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < 4; ++b) B[b] = __builtin_amdgcn_ballot_w64(((w >> (8 * b)) & 0xffu) != 0);
+  if (!a.ped_mask) return ~0u;
+  // (the lane index made opaque: the loop-invariant addresses below would be
+  // formed in the prologue and held, a spill, at the register limit)
+  int lane = c.lane;
+  asm volatile("" : "+v"(lane));
+  if (mask_one_load(a)) {   // the LDS row, addressed from the small block: no pointer of its own
+    const int l = lane < Nmax / 4 ? lane : 0;
+    return reinterpret_cast<const uint32_t*>(c.sm + (lay.o_mask - lay.o_small))[l];
   }
+  const uint8_t* pm = a.ped_mask + (size_t)c.s * Nmax;
+  uint32_t w = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int n = 4 * lane + b;
+    w |= (uint32_t)(n < Nmax ? pm[n] : 0) << (8 * b);
+  }
+  return w;
+}
+
+// Pedestrian n = 16 t + L has targets (n < n_active and its ped_mask byte
+// set): bit t of the lane's word.  The mask row comes as one dword per lane
+// (w = scene_mask_word: pedestrians 4l .. 4l + 3 in lane l) and is spread by
+// four ballots: one global round trip per wave, not one per 64 pedestrians.
+__device__ __forceinline__ unsigned scene_act_bits(const SceneCtx& c, uint32_t w) {
+  unsigned long long B[4];   // bit l: pedestrian 4 l + b has a target
+#pragma unroll
+  for (int b = 0; b < 4; ++b) B[b] = __builtin_amdgcn_ballot_w64(((w >> (8 * b)) & 0xffu) != 0);
   const int b = c.L & 3;
   const unsigned long long mine = b == 0 ? B[0] : b == 1 ? B[1] : b == 2 ? B[2] : B[3];
   unsigned bits = 0;
@@ -1203,7 +1225,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
   const int pw = c.wv - kRecW, L = c.L, q = c.q, lane = c.lane, s = c.s, ntact = c.ntact;
-  const unsigned act_bits = scene_act_bits(a, c);
+  unsigned act_bits = 0;   // formed after the first staging
   // tile items of a chunk (forward): item j -> frame j / ntact, tile
   // j % ntact; this producer takes items pw, pw + NP, ...  (GRAD: whole
   // frames per worker, grad_frames)
@@ -1228,7 +1250,8 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
-    scene_stage<64 * (kRecW + NP), NP, 0, NLL>(a, lay, c, fb, cnt, false, [] {});
+    scene_stage<64 * (kRecW + NP), NP, NLL>(a, lay, c, fb, cnt, [] {});
+    if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
     const int nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;   // forward
     // GRAD: this producer's frames pw, pw + NP, ... < gend of the chunk (the
     // last R frames of the last chunk go to the recurrence waves)
@@ -1430,7 +1453,8 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
     const int R = grad_rec_frames(cnt, NP);
     if (R > 0) {
       float2 tg[4];
-      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, cnt - R + c.wv, R, cnt, scene_act_bits(a, c),
+      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, cnt - R + c.wv, R, cnt,
+                           scene_act_bits(c, scene_mask_word(a, lay, c)),
                            acc, lsum, tg, false);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (c.lane == 0) atomicAdd(c.sGseq, 1);
@@ -1483,10 +1507,12 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
     scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first
     // the small segments: one wave each (one pointer per wave keeps the
     // kernel-argument loads off a serial s_load / s_waitcnt chain)
-    for (int seg = wv; seg < (NLL ? 11 : 10); seg += NT / 64) {
+    for (int seg = wv; seg < 12; seg += NT / 64) {
       const float* src;
       float* dst;
       int n;
+      if (seg == 10 && !NLL) continue;
+      if (seg == 11 && !mask_one_load(a)) continue;
       switch (seg) {
         case 0: src = a.w.Wi; dst = c.sWi; n = Nmax * kD; break;
         case 1: src = a.w.Wo; dst = c.sWo; n = kT * Nmax; break;
@@ -1498,7 +1524,10 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
         case 7: src = a.w.Wc; dst = c.sm + SM_WC; n = kL2 * kT; break;
         case 8: src = a.vislet + (size_t)c.s * 2 * Nmax; dst = c.sVis; n = Nmax; break;
         case 9: src = a.vislet + (size_t)c.s * 2 * Nmax + Nmax; dst = c.sVis + Nmax; n = Nmax; break;
-        default: src = a.w.head; dst = c.sNllR; n = kNllHead; break;   // NLL head [3][12]
+        case 10: src = a.w.head; dst = c.sNllR; n = kNllHead; break;   // NLL head [3][12]
+        default:                                       // the ped_mask row, dwords
+          src = reinterpret_cast<const float*>(a.ped_mask + (size_t)c.s * Nmax);
+          dst = smem + lay.o_mask; n = Nmax / 4; break;
       }
       // 16 bytes per lane when both ends allow it (every segment of the
       // usual layouts): 11 wave-instructions instead of 26 through the CU's
@@ -1518,19 +1547,24 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
       c.sMflag[c.tid] = 0;
     }
   }
-  {
+  // scene scalars: one scalar round trip (the recurrence's h and the
+  // producers' ped_mask word are loaded later, off the prologue's burst)
+  auto scalars = [&] {
     int na, nf;
     sload2_i32(a.n_active + c.s, a.n_frames ? a.n_frames + c.s : a.n_active + c.s, na, nf);
     c.nact = clampi(na, 0, Nmax);
     c.nf = a.n_frames ? clampi(nf, 0, F) : F;
-  }
-  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians
-  if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
+    c.ntact = (c.nact + 15) >> 4;                      // tiles holding active pedestrians
+    if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
+  };
   if (c.wv < kRecW) {
+    scalars();
     scene_recurrence<TPW, NP>(a, lay, c);
     if (GRAD) rec_grad_work<NP, PM, NLL>(a, lay, c);
-  } else
+  } else {
+    scalars();
     scene_producer<NP, GRAD, PM, NLL>(a, lay, c);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
 }
 

@@ -3,7 +3,9 @@ product code).  Each variant is a set of text replacements applied to a temp
 copy of multimodaltraj_2_amd/csrc; the copy is built into /tmp and timed on
 the bench workload (HIP events, reference-mode step and train step).
 
-usage: python tools/ab_time.py [CONFIG] [VARIANT ...]   (variants: see VARIANTS)"""
+usage: python tools/ab_time.py --build VARIANT ...       (CPU host: into tools/ab/)
+       python tools/ab_time.py [CONFIG] [VARIANT ...]   (GPU: timelines / times)
+       python tools/ab_time.py --rounds K [CONFIG] VARIANT ...   (interleaved A/B)"""
 import ctypes
 import os
 import shutil
@@ -37,8 +39,8 @@ P0 = "c.wv == kRecW"
 STAMPS = [
     ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
     ("int scene_step_launch(const StepArgs& a, hipStream_t st) {", "int scene_step_launch(const StepArgs& a, hipStream_t st) {\n  (void)0;"),
-    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
-     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
     ("    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});",
      "    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});\n    G2K_ST(1, " + P0 + " && fb == 0);"),
     ("    // phase 2 — predictions and errors (GRAD: and the gradient)",
@@ -83,30 +85,30 @@ TILE = [
 R0 = "c.wv == 0"
 TL_FWD = [
     ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
-    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+    ("  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
      "  G2K_ST(0, c.tid == 0);\n  if (c.wv == 0 && c.lane == 0) g2k_stamp_buf[(size_t)c.s * 64 + 27] = (unsigned)__builtin_amdgcn_s_memrealtime();\n"
-     "  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
-    ("    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
-     "    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first\n    G2K_ST(1, " + P0 + ");"),
-    ("  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians",
-     "  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians\n  G2K_ST(3, " + P0 + ");"),
-    ("  __syncthreads();                                              // B1: window + weights landed",
-     "  G2K_ST(4, " + P0 + " && fb == 0);\n  __syncthreads();\n  G2K_ST(5, " + P0 + " && fb == 0);"),
-    ("  __syncthreads();                                              // B2: V, VG, K1, K2",
-     "  G2K_ST(51, " + P0 + " && fb == 0);\n  __syncthreads();\n  G2K_ST(6, " + P0 + " && fb == 0);"),
+     "  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("    scene_pos_dma<64 * kRecW>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
+     "    scene_pos_dma<64 * kRecW>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first\n    G2K_ST(1, c.wv == 0);"),
+    ("    c.ntact = (c.nact + 15) >> 4;                      // tiles holding active pedestrians",
+     "    c.ntact = (c.nact + 15) >> 4;                      // tiles holding active pedestrians\n    G2K_ST(3, " + P0 + ");"),
+    ("  __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed",
+     "  G2K_ST(4, " + P0 + " && fb == 0);\n  __builtin_amdgcn_s_barrier();\n  G2K_ST(5, " + P0 + " && fb == 0);"),
+    ("  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2",
+     "  G2K_ST(51, " + P0 + " && fb == 0);\n  __builtin_amdgcn_s_barrier();\n  G2K_ST(6, " + P0 + " && fb == 0);"),
     ("      const FrameHeadOut hd =", "      G2K_ST(7 + 2 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n      const FrameHeadOut hd ="),
     ("      if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n", "      if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      G2K_ST(8 + 2 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n"),
     ("        poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)",
      "        G2K_ST(13 + 2 * k, " + P0 + " && k < 6);\n        poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)\n        G2K_ST(14 + 2 * k, " + P0 + " && k < 6);"),
     ("  publish_metrics(a, c, pw, GRAD ? NP + kRecW : NP, acc, lsum, GRAD);",
      "  G2K_ST(25, " + P0 + ");\n  publish_metrics(a, c, pw, GRAD ? NP + kRecW : NP, acc, lsum, GRAD);\n  G2K_ST(50, " + P0 + ");"),
-    ("        rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,\n                    as_lane + fn * kD * kD, fln, bn);",
-     "        rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,\n                    as_lane + fn * kD * kD, fln, bn);\n        G2K_ST(30 + g, " + R0 + " && g < 20);"),
+    ("        rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,\n                    as_lane + fn * kD * kD, fln, bn, g + 1 == c.nf);",
+     "        rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag + fn,\n                    as_lane + fn * kD * kD, fln, bn, g + 1 == c.nf);\n        G2K_ST(30 + g, " + R0 + " && g < 20);"),
     ("  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L,\n           c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);",
      "  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L,\n           c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);\n  G2K_ST(26, " + R0 + ");\n"
      "  if (c.wv == 0 && c.lane == 0) g2k_stamp_buf[(size_t)c.s * 64 + 28] = (unsigned)__builtin_amdgcn_s_memrealtime();"),
-    ("    scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, live, [&] {",
-     "    G2K_ST(52, " + R0 + " && fb == 0);\n    scene_stage<NT, NP, TPW * 4>(a, lay, c, fb, cnt, live, [&] {"),
+    ("      if (c.lane == 0) atomicAdd(seq + kSyncDma, 1);\n      if (live) rc.load(",
+     "      if (c.lane == 0) atomicAdd(seq + kSyncDma, 1);\n      G2K_ST(52, " + R0 + ");\n      if (live) rc.load("),
 ]
 
 
@@ -125,8 +127,8 @@ TL_REC = TL_FWD + [
 # the same stamps kept in LDS (no global store, so no vmcnt wait behind a
 # stamp) and copied out after a final barrier
 LDS_STAMP_DEF = """
-__device__ unsigned g2k_stamp_buf[4096 * 128];
-__shared__ unsigned g2k_lds_stamp[128];
+__device__ unsigned g2k_stamp_buf[4096 * 160];
+__shared__ unsigned g2k_lds_stamp[160];
 #define G2K_ST(k, cond) do { if ((cond) && (threadIdx.x & 63) == 0) { \\
   g2k_lds_stamp[(k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
 """
@@ -142,7 +144,7 @@ def lds_stamps(reps, head=True):
         out.append((a, b))
     out += [
         ('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup',
-         '  __syncthreads();\n  if (c.tid < 128) g2k_stamp_buf[(size_t)c.s * 128 + c.tid] = g2k_lds_stamp[c.tid];\n'
+         '  __syncthreads();\n  if (c.tid < 160) g2k_stamp_buf[(size_t)c.s * 160 + c.tid] = g2k_lds_stamp[c.tid];\n'
          '  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup'),
     ]
     if head:
@@ -188,14 +190,18 @@ TL_TILE = [
 
 # every wave's own DMA wait before B1 (wave w -> slot 39 + w, w >= 1)
 TL_B1 = [
-    ("  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians",
-     "  c.ntact = (c.nact + 15) >> 4;                        // tiles holding active pedestrians\n  G2K_ST(112 + c.wv, true);"),
+
+    ("    c.ntact = (c.nact + 15) >> 4;                      // tiles holding active pedestrians",
+     "    c.ntact = (c.nact + 15) >> 4;                      // tiles holding active pedestrians\n    G2K_ST(112 + c.wv, true);"),
     ("  // every kernel-argument line the prologue reads, in ONE scalar-load round",
      "  G2K_ST(80 + (threadIdx.x >> 6), true);\n  // every kernel-argument line the prologue reads, in ONE scalar-load round"),
-    ("    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
-     "    G2K_ST(96 + c.wv, true);\n    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first"),
-    ("  __syncthreads();                                              // B1: window + weights landed",
-     "  G2K_ST(64 + c.wv, fb == 0);\n  __syncthreads();                                              // B1: window + weights landed"),
+    ("    scene_pos_dma<64 * kRecW>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
+     "    G2K_ST(96 + c.wv, true);\n    scene_pos_dma<64 * kRecW>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first"),
+    ("  const int pw = c.wv - kRecW;\n  if (pw < ntask) {\n    poll_flag(sync + kSyncDma, kRecW);",
+     "  const int pw = c.wv - kRecW;\n  G2K_ST(64 + c.wv, true);\n  if (pw < ntask) {\n    poll_flag(sync + kSyncDma, kRecW);\n    G2K_ST(144 + c.wv, true);"),
+    ("  poll_flag(sync + kSyncStage, ntask);\n}", "  poll_flag(sync + kSyncStage, ntask);\n  G2K_ST(128 + c.wv, true);\n}"),
+
+
 ]
 
 
@@ -210,8 +216,8 @@ POS1K = [
 # minimal stamps: every wave's exit (slot 64 + wave), R0's start (0)
 TL_END = [
     ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
-    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
-     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
     ('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup',
      '  G2K_ST(64 + c.wv, true);\n  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup'),
 ]
@@ -333,15 +339,25 @@ VARIANTS = {
 }
 
 
+AB_DIR = os.path.join(ROOT, "tools", "ab")   # prebuilt variant libraries (git-ignored; travel to the box)
+
+
+def variant_path(name):
+    return os.path.join(AB_DIR, f"libg2k_{name}.so")
+
+
 def build_variant(name):
+    """Build variant `name` into tools/ab/libg2k_<name>.so (on the CPU host:
+    the library travels to the GPU box with the tree)."""
+    from concurrent.futures import ThreadPoolExecutor
     src = os.path.join(ROOT, "multimodaltraj_2_amd", "csrc")
     tmp = tempfile.mkdtemp(prefix=f"g2k_{name}_")
     for f in os.listdir(src):
         shutil.copy(os.path.join(src, f), tmp)
         if name == "orig" or name.endswith("_orig"):   # reference sources in tools/ab_ref (no .git on the box)
             ref = os.path.join(ROOT, "tools", "ab_ref", f)
-            assert os.path.exists(ref), "tools/ab_ref is missing: copy a committed csrc there"
-            shutil.copy(ref, os.path.join(tmp, f))
+            if os.path.exists(ref):
+                shutil.copy(ref, os.path.join(tmp, f))
     for fname, reps in VARIANTS[name].items():
         if fname == "__flags__":
             continue
@@ -353,17 +369,32 @@ def build_variant(name):
         if (name.startswith("stamps") or name.startswith("tl_")) and fname == SCENE:
             s += STAMP_EXPORT
         open(p, "w").write(s)
-    out = f"/tmp/libg2k_{name}.so"
-    objs = []
-    for f in sorted(os.listdir(tmp)):
-        if f.endswith(".hip"):
-            o = os.path.join(tmp, f[:-4] + ".o")
-            subprocess.run([build.HIPCC, *build.flags_for(f), *VARIANTS[name].get("__flags__", []), "-c", "-o", o,
-                            os.path.join(tmp, f)], check=True)
-            objs.append(o)
+    os.makedirs(AB_DIR, exist_ok=True)
+    out = variant_path(name)
+
+    def comp(f):
+        o = os.path.join(tmp, os.path.splitext(f)[0] + ".o")
+        if f.endswith(".cpp"):
+            cmd = [build.CXX, *build.CXX_FLAGS, "-c", "-o", o, os.path.join(tmp, f)]
+        else:
+            cmd = [build.HIPCC, *build.flags_for(f), *VARIANTS[name].get("__flags__", []), "-c", "-o", o,
+                   os.path.join(tmp, f)]
+        subprocess.run(cmd, check=True)
+        return o
+
+    files = sorted(f for f in os.listdir(tmp) if f.endswith(".hip") or f.endswith(".cpp"))
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        objs = list(ex.map(comp, files))
     subprocess.run([build.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs],
                    check=True)
+    shutil.rmtree(tmp, ignore_errors=True)
     return out
+
+
+def variant_lib(name):
+    """The prebuilt variant (tools/ab/), built here if missing (CPU host)."""
+    p = variant_path(name)
+    return p if os.path.exists(p) else build_variant(name)
 
 
 def time_it(fn, reps=200, warm=20):
@@ -427,7 +458,7 @@ def interleaved(cfg, names, rounds):
     batches = [t] + [make_batch(S, c["Nmax"], c["H"], seed=100 + k).to_device(dev) for k in range(1, K)]
     runs = {}
     for name in names:
-        lib = _lib.load(build_variant(name))
+        lib = _lib.load(variant_lib(name))
         _lib._lib = lib
         params = fs.init_params(c["Nmax"], seed=0, device=dev)
         plans = [fs.StepPlan(params, b["pos"], b["vislet"], b["G"], b["targets"], b["n_active"], b["h0"],
@@ -450,6 +481,12 @@ def interleaved(cfg, names, rounds):
 
 def main():
     args = sys.argv[1:]
+    if args and args[0] == "--build":      # CPU host: prebuild the named variants
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=2) as ex:
+            for out in ex.map(build_variant, [a for a in args[1:] if a in VARIANTS]):
+                print(out)
+        return
     if args and args[0] == "--rounds":
         rounds = int(args[1])
         rest = args[2:]
@@ -464,7 +501,7 @@ def main():
     b = make_batch(S, c["Nmax"], c["H"], seed=1)
     t = b.to_device(dev)
     for name in names:
-        lib = _lib.load(build_variant(name))
+        lib = _lib.load(variant_lib(name))
         _lib._lib = lib
         if name.startswith("tl_"):
             import numpy as np
@@ -488,7 +525,7 @@ def main():
                 for _ in range(5):
                     plan.run()
             torch.cuda.synchronize()
-            W = 128 if name in ("tl_lds", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig") else 64
+            W = 160 if name in ("tl_lds", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig") else 64
             buf = (ctypes.c_uint * (S * W))()
             assert lib.g2k_stamp_copy(buf, S * W) == 0
             st = np.frombuffer(buf, dtype=np.uint32).reshape(S, W).astype(np.int64)
@@ -500,10 +537,12 @@ def main():
                 print("head 0 (median): operands", int(med[60]), "A done", int(med[61]), "attn done",
                       int(med[62]))
                 if name.startswith("tl_b1"):
-                    print("B1 waits per wave (median, wave 0..11):", [int(med[64 + w]) for w in range(12)])
-                    print("wave starts (median, rel. to wave 0's stamp 0):", [int(med[80 + w]) for w in range(12)])
-                    print("wave DMA issue start (median):", [int(med[96 + w]) for w in range(12)])
-                    print("wave nact loaded (median):", [int(med[112 + w]) for w in range(12)])
+                    print("at staging (rec: DMA landed, signalled) (median, wave 0..15):", [int(med[64 + w]) for w in range(16)])
+                    print("task workers: DMA seen (median):", [int(med[144 + w]) for w in range(16)])
+                    print("wave starts (median, rel. to wave 0's stamp 0):", [int(med[80 + w]) for w in range(16)])
+                    print("wave DMA issue start (median):", [int(med[96 + w]) for w in range(16)])
+                    print("wave nact loaded (median):", [int(med[112 + w]) for w in range(16)])
+                    print("staging done seen (median):", [int(med[128 + w]) for w in range(16)])
                 if name == "tl_tile":
                     print("last tile (median): entry", int(med[40]), "Y", int(med[41]), "targets", int(med[42]),
                           "stores", int(med[43]), "errors", int(med[44]))
