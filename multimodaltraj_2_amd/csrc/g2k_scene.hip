@@ -537,12 +537,17 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   const bool live = a.h_in != nullptr;
   RecurH<TPW, kRecW> rc;
   int* seq = reinterpret_cast<int*>(c.sRed + 2 * kRB);   // 2 partial buffers, seq words, row max
+  // the first chunk's staging ahead of the chunk loop (see scene_producer)
+  if (c.nf > 0)
+    scene_stage<NT, NP>(a, lay, c, 0, c.nf < lay.fc ? c.nf : lay.fc, [&] {
+      if (live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
+    });
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
-    if (fb > 0) scene_pos_dma<NT>(a, lay, c, fb, cnt);
-    scene_stage<NT, NP>(a, lay, c, fb, cnt, [&] {
-      if (fb == 0 && live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
-    });
+    if (fb > 0) {
+      scene_pos_dma<NT>(a, lay, c, fb, cnt);
+      scene_stage<NT, NP>(a, lay, c, fb, cnt, [] {});
+    }
     if (fb == 0 && live) {
       // softmax(h) numerators: row max exchange (seq 1), then e and its row
       // partials into buffer 0 (seq 2), no workgroup barrier
@@ -1247,10 +1252,19 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   };
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float lsum = 0.f;
+  // the first chunk's staging ahead of the chunk loop: the loop's invariant
+  // code (addresses and descriptors for the heads, tiles and errors, which
+  // the compiler computes in the loop's preheader) then runs after the
+  // staging barriers, not in every producer's prologue before them (there it
+  // was ~600 instructions per wave, issued one wave after the other on a
+  // SIMD, and the first staging barrier waited for the last)
+  if (c.nf > 0) scene_stage<64 * (kRecW + NP), NP, NLL>(a, lay, c, 0, c.nf < lay.fc ? c.nf : lay.fc, [] {});
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
-    if (fb > 0) scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
-    scene_stage<64 * (kRecW + NP), NP, NLL>(a, lay, c, fb, cnt, [] {});
+    if (fb > 0) {
+      scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
+      scene_stage<64 * (kRecW + NP), NP, NLL>(a, lay, c, fb, cnt, [] {});
+    }
     if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
     const int nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;   // forward
     // GRAD: this producer's frames pw, pw + NP, ... < gend of the chunk (the

@@ -285,6 +285,7 @@ NO_RECUR = [("  const bool live = a.h_in != nullptr;", "  const bool live = fals
 NO_RECUR_SCENE = {SCENE: NO_RECUR}
 VARIANTS = {
     "base": {},
+    "prev": {},   # prebuilt only: tools/ab/libg2k_prev.so (the last commit)
     "orig": {},
     "no_finalize": {SCENE: [("  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);",
                              "  return;\n  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);")]},
