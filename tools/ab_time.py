@@ -39,8 +39,8 @@ P0 = "c.wv == kRecW"
 STAMPS = [
     ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
     ("int scene_step_launch(const StepArgs& a, hipStream_t st) {", "int scene_step_launch(const StepArgs& a, hipStream_t st) {\n  (void)0;"),
-    ("  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
-     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
     ("    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});",
      "    scene_stage<64 * (kRecW + NP), NP, 0>(a, lay, c, fb, cnt, false, [] {});\n    G2K_ST(1, " + P0 + " && fb == 0);"),
     ("    // phase 2 — predictions and errors (GRAD: and the gradient)",
@@ -85,11 +85,11 @@ TILE = [
 R0 = "c.wv == 0"
 TL_FWD = [
     ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
-    ("  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
      "  G2K_ST(0, c.tid == 0);\n  if (c.wv == 0 && c.lane == 0) g2k_stamp_buf[(size_t)c.s * 64 + 27] = (unsigned)__builtin_amdgcn_s_memrealtime();\n"
-     "  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
-    ("    scene_pos_dma<64 * kRecW>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
-     "    scene_pos_dma<64 * kRecW>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first\n    G2K_ST(1, c.wv == 0);"),
+     "  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
+     "    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first\n    G2K_ST(1, " + P0 + ");"),
     ("    c.ntact = (c.nact + 15) >> 4;                      // tiles holding active pedestrians",
      "    c.ntact = (c.nact + 15) >> 4;                      // tiles holding active pedestrians\n    G2K_ST(3, " + P0 + ");"),
     ("  __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed",
@@ -107,8 +107,8 @@ TL_FWD = [
     ("  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L,\n           c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);",
      "  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L,\n           c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);\n  G2K_ST(26, " + R0 + ");\n"
      "  if (c.wv == 0 && c.lane == 0) g2k_stamp_buf[(size_t)c.s * 64 + 28] = (unsigned)__builtin_amdgcn_s_memrealtime();"),
-    ("      if (c.lane == 0) atomicAdd(seq + kSyncDma, 1);\n      if (live) rc.load(",
-     "      if (c.lane == 0) atomicAdd(seq + kSyncDma, 1);\n      G2K_ST(52, " + R0 + ");\n      if (live) rc.load("),
+    ("      if (live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);\n    });",
+     "      if (live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);\n    });\n  G2K_ST(52, " + R0 + ");"),
 ]
 
 
@@ -195,11 +195,12 @@ TL_B1 = [
      "    c.ntact = (c.nact + 15) >> 4;                      // tiles holding active pedestrians\n    G2K_ST(112 + c.wv, true);"),
     ("  // every kernel-argument line the prologue reads, in ONE scalar-load round",
      "  G2K_ST(80 + (threadIdx.x >> 6), true);\n  // every kernel-argument line the prologue reads, in ONE scalar-load round"),
-    ("    scene_pos_dma<64 * kRecW>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
-     "    G2K_ST(96 + c.wv, true);\n    scene_pos_dma<64 * kRecW>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first"),
-    ("  const int pw = c.wv - kRecW;\n  if (pw < ntask) {\n    poll_flag(sync + kSyncDma, kRecW);",
-     "  const int pw = c.wv - kRecW;\n  G2K_ST(64 + c.wv, true);\n  if (pw < ntask) {\n    poll_flag(sync + kSyncDma, kRecW);\n    G2K_ST(144 + c.wv, true);"),
-    ("  poll_flag(sync + kSyncStage, ntask);\n}", "  poll_flag(sync + kSyncStage, ntask);\n  G2K_ST(128 + c.wv, true);\n}"),
+    ("    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first",
+     "    G2K_ST(96 + c.wv, true);\n    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first"),
+    ("  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)",
+     "  G2K_ST(128 + c.wv, fb == 0);\n  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)"),
+    ("  __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed",
+     "  G2K_ST(64 + c.wv, fb == 0);\n  __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed"),
 
 
 ]
@@ -216,8 +217,8 @@ POS1K = [
 # minimal stamps: every wave's exit (slot 64 + wave), R0's start (0)
 TL_END = [
     ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
-    ("  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
-     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kSyncStage) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
     ('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup',
      '  G2K_ST(64 + c.wv, true);\n  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup'),
 ]
@@ -538,12 +539,11 @@ def main():
                 print("head 0 (median): operands", int(med[60]), "A done", int(med[61]), "attn done",
                       int(med[62]))
                 if name.startswith("tl_b1"):
-                    print("at staging (rec: DMA landed, signalled) (median, wave 0..15):", [int(med[64 + w]) for w in range(16)])
-                    print("task workers: DMA seen (median):", [int(med[144 + w]) for w in range(16)])
+                    print("B1 waits per wave (median, wave 0..15):", [int(med[64 + w]) for w in range(16)])
                     print("wave starts (median, rel. to wave 0's stamp 0):", [int(med[80 + w]) for w in range(16)])
                     print("wave DMA issue start (median):", [int(med[96 + w]) for w in range(16)])
                     print("wave nact loaded (median):", [int(med[112 + w]) for w in range(16)])
-                    print("staging done seen (median):", [int(med[128 + w]) for w in range(16)])
+                    print("wave at staging, before its DMA wait (median):", [int(med[128 + w]) for w in range(16)])
                 if name == "tl_tile":
                     print("last tile (median): entry", int(med[40]), "Y", int(med[41]), "targets", int(med[42]),
                           "stores", int(med[43]), "errors", int(med[44]))
