@@ -301,6 +301,9 @@ def main(argv=None):
                     help="pred as [S, F, Nmax, L, 2] (the per-pedestrian view train.py:254 "
                          "transposes to; only active pedestrians written) or pred_path_band "
                          "[S, F, 2L, Nmax]")
+    ap.add_argument("--split", type=int, default=0,
+                    help="workgroups per scene (G2K_STEP_SPLIT; 0: automatic, enough to cover "
+                         "the CUs when a rank has fewer scenes than CUs)")
     ap.add_argument("--selftest-launcher", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 
@@ -344,7 +347,8 @@ def main(argv=None):
     params = params_host.to(dev)
     pbytes = sum(getattr(params, k).numel() * 4 for k in ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo"))
     shared = args.config == REAL          # real scenes: one target set per scene (every frame's)
-    layout = dict(pred_layout=args.pred_layout, targets_shared=shared, frames=F if shared else None)
+    layout = dict(pred_layout=args.pred_layout, targets_shared=shared, frames=F if shared else None,
+                  split=args.split)
     abytes = algorithmic_bytes(b, H, pbytes, shared)
     K = args.rotate or max(1, -(-MALL_BYTES // abytes) + 1)
 
@@ -411,7 +415,7 @@ def main(argv=None):
                        "frames_per_step": b.frames, "obs_len": 8, "pred_len": 12, "Nmax": Nmax,
                        "hidden": H, "D": 16, "parallelism": f"dp{world}",
                        "input_batches_rotated": K, "pred_layout": args.pred_layout,
-                       "targets_shared": shared},
+                       "targets_shared": shared, "workgroups_per_scene": split_of(S, F, args.split)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": load_pmc(args.config),
@@ -431,6 +435,12 @@ def main(argv=None):
     if dist is not None:
         dist.destroy_process_group()
     return 0
+
+
+def split_of(S, F, requested):
+    """Workgroups per scene the launch uses (scene_split, csrc/g2k_common.h)."""
+    x = requested or (1 if S >= 256 else 256 // max(S, 1))
+    return max(1, min(x, 4, max(F, 1)))
 
 
 def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, layout):

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define G2K_ABI_VERSION 3
+#define G2K_ABI_VERSION 4
 
 enum {
   G2K_OK = 0,
@@ -74,6 +74,16 @@ typedef struct g2k_dims {
  * instead of 1/2 the squared error; the gradient then covers the head too
  * (P = 24 Nmax + 496 + 36, the head's 36 after Wo). */
 #define G2K_STEP_LOSS_NLL 4
+/* Workgroups per scene (bits 8..10): G2K_STEP_SPLIT(x), x in 1..4, or 0 =
+ * automatic (x = min(4, 256 / S), at most F: a launch of fewer scenes than
+ * the device has CUs spreads each scene's frames over x workgroups, the
+ * first of which also runs the recurrence).  x > 1 needs the workspace
+ * (g2k_step_workspace_bytes / g2k_train_workspace_bytes /
+ * g2k_grad_workspace_bytes) zero-filled before its first use; every call
+ * leaves it zero-filled again. */
+#define G2K_STEP_SPLIT_SHIFT 8
+#define G2K_STEP_SPLIT_MASK (7 << G2K_STEP_SPLIT_SHIFT)
+#define G2K_STEP_SPLIT(x) ((x) << G2K_STEP_SPLIT_SHIFT)
 
 /* Model parameters (device pointers). Shapes as in the reference. */
 typedef struct g2k_weights {

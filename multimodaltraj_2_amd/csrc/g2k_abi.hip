@@ -37,6 +37,9 @@ int validate_common(const g2k_dims* d, bool need_F, bool any_D = false, int flag
   if (!d) return set_err(G2K_EINVAL, "dims is NULL");
   if (d->flags & ~flags_ok)
     return set_err(G2K_EUNSUPPORTED, "flags 0x%x not supported by this entry point", d->flags);
+  if (((d->flags & G2K_STEP_SPLIT_MASK) >> G2K_STEP_SPLIT_SHIFT) > kMaxSplit)
+    return set_err(G2K_EINVAL, "G2K_STEP_SPLIT(%d): at most %d workgroups per scene",
+                   (d->flags & G2K_STEP_SPLIT_MASK) >> G2K_STEP_SPLIT_SHIFT, kMaxSplit);
   if (d->T != kT || d->L != kL)
     return set_err(G2K_EUNSUPPORTED, "unsupported geometry T=%d L=%d (need 8/12)", d->T, d->L);
   if (any_D ? (d->D < 1 || d->D > kD) : d->D != kD)
@@ -71,7 +74,7 @@ int validate_step_inputs(const g2k_dims* d, const g2k_weights* w, const float* p
                          const int32_t* n_active, bool train = false) {
   int rc = validate_common(d, true, false,
                            G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED |
-                               (train ? G2K_STEP_LOSS_NLL : 0));
+                               G2K_STEP_SPLIT_MASK | (train ? G2K_STEP_LOSS_NLL : 0));
   if (rc) return rc;
   if ((rc = validate_weights(w, true))) return rc;
   if (d->stride < 0) return set_err(G2K_EINVAL, "stride=%d < 0", d->stride);
@@ -93,9 +96,11 @@ StepArgs step_args(const g2k_dims* d, const g2k_weights* w, const float* pos, co
   return a;
 }
 
-// [S][P + 2] gradient rows, then one 64-byte line for the update ticket
+// [S * X][P + 2] gradient rows (one per workgroup), one 64-byte line for the
+// update ticket, then the split workspace (scene tickets, metric partials)
 int64_t grad_rows_bytes(const g2k_dims* d) {
-  return (int64_t)d->S * (grad_params(d->Nmax, loss_nll(*d)) + 2) * 4 + 64;
+  return (int64_t)d->S * scene_split(*d) * (grad_params(d->Nmax, loss_nll(*d)) + 2) * 4 + 64 +
+         split_ws_bytes(*d);
 }
 
 // train mode after the inputs are validated: the fused step with gradient
@@ -118,12 +123,15 @@ int train_launch(StepArgs a, float* grad, void* workspace, int64_t workspace_byt
     if (params) return update_launch(params, ms, grad, width - 2, lr, decay, grad_clip, st);
     return G2K_OK;
   }
+  const int nrows = a.d.S * scene_split(a.d);
   a.grad_rows = static_cast<float*>(workspace);
-  a.grad_ticket = params ? reinterpret_cast<int*>(a.grad_rows + (size_t)a.d.S * width) : nullptr;
+  int* line = reinterpret_cast<int*>(a.grad_rows + (size_t)nrows * width);
+  a.grad_ticket = params ? line : nullptr;
+  split_ws_bind(a, line + 16);
   if ((rc = scene_step_launch(a, st))) return rc;
-  if (!params) return grad_rows_launch(a.grad_rows, a.d.S, width, grad, st);
+  if (!params) return grad_rows_launch(a.grad_rows, nrows, width, grad, st);
   const UpdateArgs up{params, ms, lr, decay, grad_clip, a.grad_ticket};
-  return grad_rows_launch(a.grad_rows, a.d.S, width, grad, st, &up);
+  return grad_rows_launch(a.grad_rows, nrows, width, grad, st, &up);
 }
 
 }  // namespace
@@ -140,7 +148,7 @@ int g2k_abi_version(void) { return G2K_ABI_VERSION; }
 
 const char* g2k_last_error(void) { return g_err; }
 
-constexpr int kStepFlags = G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED;
+constexpr int kStepFlags = G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED | G2K_STEP_SPLIT_MASK;
 constexpr int kTrainFlags = kStepFlags | G2K_STEP_LOSS_NLL;
 
 int64_t g2k_step_lds_bytes(const g2k_dims* d) {
@@ -150,7 +158,7 @@ int64_t g2k_step_lds_bytes(const g2k_dims* d) {
 
 int64_t g2k_step_workspace_bytes(const g2k_dims* d) {
   if (validate_common(d, true, false, kStepFlags) != G2K_OK) return -1;
-  return 0;   // the fused step keeps every intermediate on chip
+  return split_ws_bytes(*d);   // one workgroup per scene: every intermediate stays on chip
 }
 
 int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
@@ -159,7 +167,6 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
                        const uint8_t* ped_mask, const float* h_in, float* h_out, float* pred,
                        float* metrics, float* A_out, float* cost_out, float lambda,
                        void* workspace, int64_t workspace_bytes, void* stream) {
-  (void)workspace;
   int rc = validate_step_inputs(d, w, pos, vislet, G, targets, n_active);
   if (rc) return rc;
   if ((rc = validate_H(d->H))) return rc;
@@ -169,9 +176,14 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
     return set_err(G2K_EINVAL, "h_in and h_out must be 16-byte aligned");
   if (workspace_bytes < 0) return set_err(G2K_EINVAL, "negative workspace size");
   if (d->S == 0) return G2K_OK;
+  const int64_t need = split_ws_bytes(*d);
+  if (need > 0 && (!workspace || workspace_bytes < need))
+    return set_err(G2K_EINVAL, "workspace of %lld bytes needed (got %lld)", (long long)need,
+                   (long long)workspace_bytes);
   StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda);
   a.h_in = h_in; a.h_out = h_out; a.pred = pred; a.metrics = metrics; a.A_out = A_out;
   a.cost_out = cost_out;
+  split_ws_bind(a, workspace);
   return scene_step_launch(a, (hipStream_t)stream);
 }
 

@@ -393,10 +393,36 @@ struct StepArgs {
   float* A_out;
   float* cost_out;
   float lambda;
-  float* grad_rows;   // [S][P + 2] or NULL
+  float* grad_rows;   // [S * X][P + 2] or NULL (X = scene_split: one row per workgroup)
   int* grad_ticket;   // train step with update: zeroed by workgroup 0 for the gradient-row
                       // sum's last-workgroup count (g2k_train.hip), or NULL
+  int* scene_ticket;  // X > 1: [S] workgroups of a scene done (zero between launches)
+  float* met_part;    // X > 1: [S][X][8] the workgroups' metric partials
 };
+
+// Workgroups per scene of the fused step (G2K_STEP_SPLIT, include/g2k_hip.h):
+// the requested count, else enough to cover the device's 256 CUs (4 at most),
+// never more than the frames to share.
+constexpr int kSceneCUs = 256;
+constexpr int kMaxSplit = 4;
+inline int scene_split(const g2k_dims& d) {
+  int x = (d.flags & G2K_STEP_SPLIT_MASK) >> G2K_STEP_SPLIT_SHIFT;
+  if (x == 0) x = d.S >= kSceneCUs ? 1 : (d.S > 0 ? kSceneCUs / d.S : 1);
+  if (x > kMaxSplit) x = kMaxSplit;
+  if (x > d.F) x = d.F;
+  return x < 1 ? 1 : x;
+}
+// split workspace: the scene tickets (one 64-byte line per 16 scenes), then the partials
+inline int64_t split_ws_bytes(const g2k_dims& d) {
+  const int x = scene_split(d);
+  if (x <= 1) return 0;
+  return (int64_t)((d.S + 15) / 16) * 64 + (int64_t)d.S * x * 8 * 4;
+}
+inline void split_ws_bind(StepArgs& a, void* ws) {
+  if (scene_split(a.d) <= 1) { a.scene_ticket = nullptr; a.met_part = nullptr; return; }
+  a.scene_ticket = static_cast<int*>(ws);
+  a.met_part = reinterpret_cast<float*>(static_cast<char*>(ws) + (int64_t)((a.d.S + 15) / 16) * 64);
+}
 int scene_step_launch(const StepArgs& a, hipStream_t st);
 int64_t scene_lds_bytes(const g2k_dims* d, bool grad);
 

@@ -68,6 +68,7 @@ struct SceneLayout {
   // its per-step constants [5][12] (1/sigma_x, 1/sigma_y, rho, 1/(1-rho^2), base)
   int o_nlla, o_nllw, o_nllr, o_nllc;
   int tfb;             // target bytes per frame (0: one set for every frame, G2K_STEP_TARGETS_SHARED)
+  int split;           // workgroups per scene (scene_split): workgroup x owns the frames g = x mod split
   int total;           // floats
 };
 
@@ -75,6 +76,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
                                                        bool grad, bool nll = false) {
   SceneLayout s;
   s.fc = fc;
+  s.split = 1;
   s.tfb = Nmax * kL2 * 4;
   s.wcmax = (fc - 1) * stride + kT;
   s.pp = 2 * Nmax;                            // unpadded: the chunk's rows are one contiguous copy
@@ -126,7 +128,19 @@ __host__ inline SceneLayout scene_layout(const g2k_dims* d, int NP, bool grad) {
     l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad, nll);
   }
   l.tfb = (d->flags & G2K_STEP_TARGETS_SHARED) ? 0 : d->Nmax * kL2 * 4;
+  l.split = scene_split(*d);
   return l;
+}
+
+// The frames of chunk [fb, fb + cnt) a workgroup owns (global frames g with
+// g mod split == x): local frames fo + split * i, i < n.
+struct OwnFrames {
+  int fo, n;
+};
+__device__ __forceinline__ OwnFrames own_frames(int fb, int cnt, int split, int x) {
+  int fo = x - fb % split;
+  if (fo < 0) fo += split;
+  return OwnFrames{fo, fo < cnt ? (cnt - fo + split - 1) / split : 0};
 }
 
 // frame head output: the x / y row tiles of M^T
@@ -226,7 +240,8 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
                                                    const float* sVG, int wrow0, int wcmax,
                                                    const float (&rm)[4], float lam, float* as_dst,
                                                    int* as_flag, int flag_val, float* A_g,
-                                                   float* cost_g, float* cost_l, int L, int q) {
+                                                   float* cost_g, float* cost_l, int L, int q,
+                                                   bool want_m = true) {
   // every operand load is unconditional (clamped addresses) and issued
   // before the first MFMA; the lanes' selects follow (an exec-masked load
   // would cost its own LDS round trip on the chain)
@@ -285,10 +300,12 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
   FrameHeadOut o;
   o.mT0 = f32x4{0.f, 0.f, 0.f, 0.f};
   o.mT1 = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (want_m) {   // (wave-uniform: a frame another workgroup of the scene predicts needs no M)
 #pragma unroll
-  for (int ks = 0; ks < 3; ++ks) {
-    o.mT0 = mfma4(va[ks], bx[ks], o.mT0);   // M[L][4q+i]       (x rows)
-    o.mT1 = mfma4(va[ks], by[ks], o.mT1);   // M[12+L][4q+i]    (y rows)
+    for (int ks = 0; ks < 3; ++ks) {
+      o.mT0 = mfma4(va[ks], bx[ks], o.mT0);   // M[L][4q+i]       (x rows)
+      o.mT1 = mfma4(va[ks], by[ks], o.mT1);   // M[12+L][4q+i]    (y rows)
+    }
   }
   if (A_g) {
 #pragma unroll
@@ -318,7 +335,7 @@ struct SceneCtx {
   int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
   int* sGseq;     // train: [0] producers done with the chunk's frames (cumulative), [2 + t]
                   // frames added to dWo tile t (dwo_seq)
-  int s, tid, lane, wv, L, q, nact, nf, ntiles, ntact;
+  int s, x, X, tid, lane, wv, L, q, nact, nf, ntiles, ntact;   // x: this workgroup of the scene's X
   float *sNllA, *sNllW, *sNllR, *sNllC;   // NLL loss (see SceneLayout)
 };
 
@@ -534,7 +551,7 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   constexpr int NT = 64 * (kRecW + NP);
   constexpr int kRB = 16 * kRecW;
   const int H = a.d.H;
-  const bool live = a.h_in != nullptr;
+  const bool live = a.h_in != nullptr && c.x == 0;   // (the scene's first workgroup)
   RecurH<TPW, kRecW> rc;
   int* seq = reinterpret_cast<int*>(c.sRed + 2 * kRB);   // 2 partial buffers, seq words, row max
   // the first chunk's staging ahead of the chunk loop (see scene_producer)
@@ -1131,6 +1148,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
   f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   for (int fl = f0; fl < fend; fl += fstep) {
     const int f = fb + fl;
+    const int ford = f / lay.split;                      // the workgroup's own frames in order (dwo_seq)
     poll_flag(c.sMflag + fl, f + 1);                     // M of this frame (a producer's head)
     const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)c.s * F + f) * kL2 * Nmax : a.targets,
                                 a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
@@ -1146,7 +1164,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
       // to in frame order (tile sequence word) when that is too big
       const int nb = 16 * t + 4 * q;
       float* dst = c.sGdWo + (lay.dwo_seq ? 0 : slot * Nmax * kT);
-      if (lay.dwo_seq) poll_word(c.sGseq + 2 + t, f);
+      if (lay.dwo_seq) poll_word(c.sGseq + 2 + t, ford);
       if (L < kT) {
 #pragma unroll
         for (int v = 0; v < 4; ++v)
@@ -1154,7 +1172,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
       }
       if (lay.dwo_seq) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (c.lane == 0) lds_store_flag(c.sGseq + 2 + t, f + 1);
+        if (c.lane == 0) lds_store_flag(c.sGseq + 2 + t, ford + 1);
       }
     }
     // the frame's dM to this worker's scratch (M's physical rows), then its terms
@@ -1212,16 +1230,38 @@ __device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCt
     ticket = atomicAdd(c.sTicket, 1);
   }
   ticket = __builtin_amdgcn_readfirstlane(ticket);
-  if (ticket == nrows - 1 && lane < 8 && a.metrics) {
-    float v = 0.f;
-    if (lane < 5) {
-      if (c.nf > 0)
-        for (int p = 0; p < nrows; ++p) v += c.sMet[p * 8 + lane];
-    } else if (lane == 5) {
-      v = (float)c.nf;
-    }
-    a.metrics[(size_t)c.s * 8 + lane] = v;
+  if (ticket != nrows - 1 || !a.metrics) return;
+  const int l8 = lane < 8 ? lane : 7;
+  float v = 0.f;
+  if (lane < 5) {
+    if (c.nf > 0)
+      for (int p = 0; p < nrows; ++p) v += c.sMet[p * 8 + lane];
+  } else if (lane == 5) {
+    v = (float)c.nf;
   }
+  if (a.met_part) {
+    // split scene: this workgroup's row into the scene's partials (stores that
+    // write through to the coherence point, completed before the ticket); the
+    // workgroup drawing the scene's last ticket sums the rows in workgroup
+    // order (deterministic) after an acquire fence, writes the metrics row and
+    // re-arms the ticket for the next launch
+    const int X = c.X, x = c.x;
+    float* part = a.met_part + (size_t)c.s * X * 8;
+    if (lane < 8) __hip_atomic_store(part + x * 8 + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0)
+      old = __hip_atomic_fetch_add(a.scene_ticket + c.s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_readfirstlane(old) != X - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (lane < 5) {
+      v = 0.f;
+      for (int p = 0; p < X; ++p)
+        v += __hip_atomic_load(part + p * 8 + l8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) __hip_atomic_store(a.scene_ticket + c.s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (lane < 8) a.metrics[(size_t)c.s * 8 + lane] = v;
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
@@ -1236,11 +1276,15 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   // frames per worker, grad_frames)
   // item j -> (j / ntact, j % ntact) by a reciprocal, no division per item
   // (exact while j * ntact < 2^16; here j < 32 ntact and ntact <= 16)
+  // Split scenes: items run over the workgroup's own frames of the chunk
+  // (local frame ofo + X i for own-frame ordinal i = j / ntact).
   const uint32_t inv = 65536u / (uint32_t)(ntact > 0 ? ntact : 1) + 1u;
+  int ofo = 0;
   auto item_ft = [&](int k, int& fl, int& t) {
     const int j = pw + k * NP;
-    fl = (int)(((uint32_t)j * inv) >> 16);
-    t = j - fl * ntact;
+    const int i = (int)(((uint32_t)j * inv) >> 16);
+    t = j - i * ntact;
+    fl = ofo + c.X * i;
   };
   const brsrc tgr = scene_targets_rsrc(a, s);
   float2 tgA[4] = {}, tgB[4] = {};
@@ -1266,15 +1310,18 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       scene_stage<64 * (kRecW + NP), NP, NLL>(a, lay, c, fb, cnt, [] {});
     }
     if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
-    const int nitems = cnt * ntact > pw ? (cnt * ntact - pw + NP - 1) / NP : 0;   // forward
-    // GRAD: this producer's frames pw, pw + NP, ... < gend of the chunk (the
-    // last R frames of the last chunk go to the recurrence waves)
-    const int R = GRAD && fb + lay.fc >= c.nf ? grad_rec_frames(cnt, NP) : 0;
-    const int gend = cnt - R;
+    const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
+    ofo = own.fo;
+    const int nitems = own.n * ntact > pw ? (own.n * ntact - pw + NP - 1) / NP : 0;   // forward
+    // GRAD: this producer's own frames (ordinals) pw, pw + NP, ... < gend of
+    // the chunk (the last R own frames of the last chunk go to the
+    // recurrence waves)
+    const int R = GRAD && fb + lay.fc >= c.nf ? grad_rec_frames(own.n, NP) : 0;
+    const int gend = own.n - R;
     // the first tiles' targets: in flight during the heads (GRAD: one buffer
     // and the balancing stores, see grad_frames)
     if (GRAD) {
-      load_targets(tgr, Nmax, c.nact, fb, pw, 0, pw < gend, L, q, tgA, lay.tfb);
+      load_targets(tgr, Nmax, c.nact, fb, own.fo + c.X * pw, 0, pw < gend, L, q, tgA, lay.tfb);
       balance_stores<PM>(a);
     } else {
       load_item(fb, nitems, 0, tgA);
@@ -1295,27 +1342,37 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     }
     // phase 1 — the critical path: frame heads in frame order, As and M into
     // the rings, then the frame's flags; the first heads the recurrence will
-    // wait for get the issue priority
-    for (int fl = pw; fl < cnt; fl += NP) {
+    // wait for get the issue priority.  The workgroup running the recurrence
+    // forms every frame's head (As), the others only their own frames'; M
+    // (and A / cost out) only for own frames.
+    const bool all_heads = a.h_in != nullptr && c.x == 0;
+    const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : c.X, nh = all_heads ? cnt : own.n;
+    for (int i = pw; i < nh; i += NP) {
+      const int fl = hb + hs * i;
       const int f = fb + fl;
+      const bool mine = !all_heads || c.X == 1 || f % c.X == c.x;
       if (fl < kRecW) __builtin_amdgcn_s_setprio(1);
       const FrameHeadOut hd =
           frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
-                     c.sFlag + fl, f + 1, a.A_out ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
-                     a.cost_out ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr,
-                     GRAD ? c.sCost + fl * kT * kT : nullptr, L, q);
-      if (L < kL && q < 2) {
-        float* m = c.sMring + fl * kL2 * kT;
-        *reinterpret_cast<float4*>(m + L * kT + 4 * q) = make_float4(hd.mT0[0], hd.mT0[1], hd.mT0[2], hd.mT0[3]);
-        *reinterpret_cast<float4*>(m + (kL + L) * kT + 4 * q) = make_float4(hd.mT1[0], hd.mT1[1], hd.mT1[2], hd.mT1[3]);
+                     c.sFlag + fl, f + 1,
+                     a.A_out && mine ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
+                     a.cost_out && mine ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr,
+                     GRAD ? c.sCost + fl * kT * kT : nullptr, L, q, mine);
+      if (mine) {
+        if (L < kL && q < 2) {
+          float* m = c.sMring + fl * kL2 * kT;
+          *reinterpret_cast<float4*>(m + L * kT + 4 * q) = make_float4(hd.mT0[0], hd.mT0[1], hd.mT0[2], hd.mT0[3]);
+          *reinterpret_cast<float4*>(m + (kL + L) * kT + 4 * q) = make_float4(hd.mT1[0], hd.mT1[1], hd.mT1[2], hd.mT1[3]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);
       __builtin_amdgcn_s_setprio(0);
     }
     // phase 2 — predictions and errors (GRAD: and the gradient)
     if (GRAD) {
-      grad_frames<PM, NLL>(a, lay, c, pw, fb, pw, NP, gend, act_bits, acc, lsum, tgA, true);
+      grad_frames<PM, NLL>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
+                           act_bits, acc, lsum, tgA, true);
       // every worker done with the chunk's frames -> its dU rows into dV
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) atomicAdd(c.sGseq, 1);
@@ -1359,7 +1416,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   if (lane == 0) atomicAdd(c.sGseq + 1, 1);
   poll_word(c.sGseq + 1, NP);
   const int P = grad_params(Nmax, NLL);
-  float* row = a.grad_rows + (size_t)s * (P + 2);
+  float* row = a.grad_rows + ((size_t)s * c.X + c.x) * (P + 2);   // this workgroup's row
   const float* ga = c.sGAcc;
   const float* sm = c.sm;
   const int o_wii = Nmax * kD, o_wv = o_wii + kD * kT, o_bv = o_wv + kT * (kD + 2),
@@ -1464,10 +1521,12 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
   if (c.nf > 0) {
     const int fb = ((c.nf - 1) / lay.fc) * lay.fc;
     const int cnt = c.nf - fb;
-    const int R = grad_rec_frames(cnt, NP);
+    const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
+    const int R = grad_rec_frames(own.n, NP);
     if (R > 0) {
       float2 tg[4];
-      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, cnt - R + c.wv, R, cnt,
+      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, own.fo + c.X * (own.n - R + c.wv), c.X * R,
+                           own.fo + c.X * own.n,
                            scene_act_bits(c, scene_mask_word(a, lay, c)),
                            acc, lsum, tg, false);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1490,7 +1549,9 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
                "s"(a.h_in), "s"(a.w.Wi), "s"(a.w.Wo), "s"(a.d.Nmax), "s"(a.d.F), "s"(a.d.W),
                "s"(a.d.stride), "s"(lay.fc), "s"(lay.pp), "s"(lay.o_pos));
   SceneCtx c;
-  c.s = blockIdx.x;
+  c.X = lay.split;
+  c.s = lay.split == 1 ? (int)blockIdx.x : (int)blockIdx.x / lay.split;
+  c.x = (int)blockIdx.x - c.s * lay.split;
   c.tid = threadIdx.x; c.lane = c.tid & 63; c.wv = wave_id(); c.L = c.lane & 15; c.q = c.lane >> 4;
   const int Nmax = a.d.Nmax, F = a.d.F;
   c.ntiles = (Nmax + 15) >> 4;
@@ -1512,7 +1573,7 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
   if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket
   if (GRAD) {                                          // accumulators and their sequence words
     for (int i = c.tid; i < lay.o_gseq + rup4(2 + c.ntiles) - lay.o_gacc; i += NT) smem[lay.o_gacc + i] = 0.f;
-    if (a.grad_ticket && c.s == 0 && c.tid == 0) *a.grad_ticket = 0;   // this step's update ticket
+    if (a.grad_ticket && blockIdx.x == 0 && c.tid == 0) *a.grad_ticket = 0;   // this step's update ticket
   }
   if (F > 0) {
     // issued before n_active / n_frames arrive: the first chunk's window for
@@ -1599,7 +1660,7 @@ int scene_producers(int H, int Nmax, bool grad) {
 
 template <int TPW, int NP, bool GRAD, bool PM>
 void launch_kp(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
-  const dim3 grid(a.d.S), block(64 * (kRecW + NP));
+  const dim3 grid(a.d.S * l.split), block(64 * (kRecW + NP));
   const size_t lds = (size_t)l.total * 4;
   if (GRAD && loss_nll(a.d))
     hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, GRAD>), grid, block, lds, st, a, l);

@@ -98,18 +98,22 @@ def _stream(stream):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-def step_flags(pred_layout="band", targets_shared=False, loss="l2") -> int:
+def step_flags(pred_layout="band", targets_shared=False, loss="l2", split=0) -> int:
     """g2k_dims.flags: pred_layout "band" = pred_path_band [S, F, 2L, Nmax],
     "ped" = pedestrian-major [S, F, Nmax, L, 2]; targets_shared = one
     [S, 1, Nmax, L, 2] target set for every frame; loss (train mode) "l2" =
-    1/2 the squared error, "nll" = the bivariate-Gaussian NLL (params.head)."""
+    1/2 the squared error, "nll" = the bivariate-Gaussian NLL (params.head);
+    split = workgroups per scene (0: automatic, G2K_STEP_SPLIT)."""
     if pred_layout not in ("band", "ped"):
         raise ValueError(f"pred_layout {pred_layout!r}: 'band' or 'ped'")
     if loss not in ("l2", "nll"):
         raise ValueError(f"loss {loss!r}: 'l2' or 'nll'")
+    if not 0 <= int(split) <= _lib.STEP_MAX_SPLIT:
+        raise ValueError(f"split {split}: 0 (automatic) .. {_lib.STEP_MAX_SPLIT}")
     return ((_lib.STEP_PRED_PED_MAJOR if pred_layout == "ped" else 0)
             | (_lib.STEP_TARGETS_SHARED if targets_shared else 0)
-            | (_lib.STEP_LOSS_NLL if loss == "nll" else 0))
+            | (_lib.STEP_LOSS_NLL if loss == "nll" else 0)
+            | (int(split) << _lib.STEP_SPLIT_SHIFT))
 
 
 def pred_shape(S, F, Nmax, pred_layout="band"):
@@ -145,24 +149,16 @@ def step_workspace_bytes(S, F, H, Nmax, W, stride) -> int:
     return int(lib.g2k_step_workspace_bytes(ctypes.byref(d)))
 
 
-_WS = {}
-
-
-def _workspace(nbytes, device):
-    """Per-device reusable workspace (grown on demand, allocated outside any
-    timed region after the first call)."""
-    key = (device.type, device.index)
-    buf = _WS.get(key)
-    if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
-        _WS[key] = buf
-    return buf
+def workspace(nbytes, device):
+    """A launch plan's own workspace, zero-filled (split scenes keep per-scene
+    tickets in it that every call leaves at zero; include/g2k_hip.h)."""
+    return torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
 def step_fused(params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
                ped_mask=None, stride=1, lam=LAMBDA, out: StepOutputs | None = None,
                want_attn=False, stream=None, h_out=None, pred_layout="band",
-               targets_shared=False, frames=None) -> StepOutputs:
+               targets_shared=False, frames=None, split=0) -> StepOutputs:
     """One pass of the per-frame body of train.py:197-276 over S scenes.
 
     pos [S, W, Nmax, 2], vislet [S, 2, Nmax], G [S, D, T],
@@ -173,7 +169,7 @@ def step_fused(params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_fra
     plan = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
                     ped_mask=ped_mask, stride=stride, lam=lam, out=out, want_attn=want_attn,
                     stream=stream, h_out=h_out, pred_layout=pred_layout,
-                    targets_shared=targets_shared, frames=frames)
+                    targets_shared=targets_shared, frames=frames, split=split)
     plan.run()
     return plan.out
 
@@ -188,10 +184,10 @@ class StepPlan:
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
                  n_frames=None, ped_mask=None, stride=1, lam=LAMBDA,
                  out: StepOutputs | None = None, want_attn=False, stream=None, h_out=None,
-                 pred_layout="band", targets_shared=False, frames=None):
+                 pred_layout="band", targets_shared=False, frames=None, split=0):
         self._fn, self._args, self.out, self._keep = _prepare_step(
             params, pos, vislet, G, targets, n_active, h, n_frames, ped_mask, stride, lam, out,
-            want_attn, stream, h_out, pred_layout, targets_shared, frames)
+            want_attn, stream, h_out, pred_layout, targets_shared, frames, split)
 
     def run(self) -> StepOutputs:
         rc = self._fn(*self._args)
@@ -211,7 +207,7 @@ def step_frames(targets, targets_shared, frames):
 
 def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_mask, stride, lam,
                   out, want_attn, stream, h_out, pred_layout="band", targets_shared=False,
-                  frames=None):
+                  frames=None, split=0):
     lib = _lib.load()
     dev = pos.device
     if dev.type != "cuda":
@@ -219,7 +215,7 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
     S, W, Nmax, two = pos.shape
     if two != 2:
         raise ValueError(f"pos: last dim {two}, expected 2")
-    flags = step_flags(pred_layout, targets_shared)
+    flags = step_flags(pred_layout, targets_shared, split=split)
     F = step_frames(targets, targets_shared, frames)
     H = int(h.shape[2])
     params.check(dev)
@@ -259,7 +255,7 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
     nws = int(lib.g2k_step_workspace_bytes(ctypes.byref(d)))
     if nws < 0:
         _lib.check("g2k_step_workspace_bytes", -1)
-    ws = _workspace(nws, dev)
+    ws = workspace(nws, dev)
     args = (ctypes.byref(d), ctypes.byref(w), _ptr(pos), _ptr(vislet), _ptr(G), _ptr(targets),
             _ptr(n_active), _ptr(n_frames), _ptr(ped_mask), _ptr(h), _ptr(out.h), _ptr(out.pred),
             _ptr(out.metrics), _ptr(out.attn), _ptr(out.cost), ctypes.c_float(lam),

@@ -24,7 +24,7 @@ import torch.distributed as dist
 from . import _lib
 from .dist import allreduce_grad
 from .frame_step import (HIDDEN_LEN, LAMBDA, OBS_LEN, PRED_LEN, G2KParams, StepPlan, _check_dev,
-                         _ptr, _stream, step_flags, step_frames)
+                         _ptr, _stream, step_flags, step_frames, workspace)
 
 GRAD_ORDER = ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo")   # g2k_weights order
 NLL_HEAD = 3 * PRED_LEN          # loss "nll": the head [3, L] follows Wo in the flat vector
@@ -65,7 +65,7 @@ class GradPlan:
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, *, n_frames=None,
                  ped_mask=None, stride=1, lam=LAMBDA, grad=None, stream=None,
-                 targets_shared=False, frames=None, loss="l2"):
+                 targets_shared=False, frames=None, loss="l2", split=0):
         lib = _lib.load()
         dev = pos.device
         if dev.type != "cuda":
@@ -91,7 +91,7 @@ class GradPlan:
         if loss == "nll" and params.head is None:
             raise ValueError('loss "nll" needs params.head [3, 12]')
         d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 64, Nmax, W, stride,
-                         step_flags("band", targets_shared, loss))
+                         step_flags("band", targets_shared, loss, split))
         P = int(lib.g2k_grad_size(ctypes.byref(d)))
         nws = int(lib.g2k_grad_workspace_bytes(ctypes.byref(d)))
         if P < 0 or nws < 0:
@@ -99,7 +99,7 @@ class GradPlan:
         self.P = P
         self.grad = grad if grad is not None else torch.empty(P + 2, device=dev,
                                                               dtype=torch.float32)
-        self._ws = torch.empty(max(nws, 256), dtype=torch.uint8, device=dev)
+        self._ws = workspace(nws, dev)
         w = params.abi()
         self._fn = lib.g2k_step_grad_f32
         self._fused = lib.g2k_step_grad_update_f32
@@ -154,25 +154,26 @@ class TrainPlan:
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
                  ped_mask=None, stride=1, lam=LAMBDA, out=None, grad=None, stream=None,
-                 pred_layout="band", targets_shared=False, frames=None, loss="l2"):
+                 pred_layout="band", targets_shared=False, frames=None, loss="l2", split=0):
         lib = _lib.load()
         if loss == "nll" and params.head is None:
             raise ValueError('loss "nll" needs params.head [3, 12]')
         self.fwd = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
                             ped_mask=ped_mask, stride=stride, lam=lam, out=out, stream=stream,
-                            pred_layout=pred_layout, targets_shared=targets_shared, frames=frames)
+                            pred_layout=pred_layout, targets_shared=targets_shared, frames=frames,
+                            split=split)
         dev = pos.device
         S, W, Nmax, _ = pos.shape
         F, H = step_frames(targets, targets_shared, frames), int(h.shape[2])
         d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride,
-                         step_flags(pred_layout, targets_shared, loss))
+                         step_flags(pred_layout, targets_shared, loss, split))
         self.P = int(lib.g2k_grad_size(ctypes.byref(d)))
         nws = int(lib.g2k_train_workspace_bytes(ctypes.byref(d)))
         if self.P < 0 or nws < 0:
             _lib.check("g2k_train_workspace_bytes", -1)
         self.grad = grad if grad is not None else torch.empty(self.P + 2, device=dev,
                                                               dtype=torch.float32)
-        self._ws = torch.empty(max(nws, 256), dtype=torch.uint8, device=dev)
+        self._ws = workspace(nws, dev)
         o = self.fwd.out
         w = params.abi()
         self._fn = lib.g2k_train_step_f32
@@ -216,9 +217,9 @@ class TrainStep:
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
                  lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,
                  n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None,
-                 pred_layout="band", targets_shared=False, frames=None, loss="l2"):
+                 pred_layout="band", targets_shared=False, frames=None, loss="l2", split=0):
         self._layout = dict(pred_layout=pred_layout, targets_shared=targets_shared, frames=frames,
-                            loss=loss)
+                            loss=loss, split=split)
         self.flat, self.params = flat_params(params, loss)
         self.P = self.flat.numel()
         self.ms = torch.ones_like(self.flat) if rmsprop else None

@@ -49,17 +49,37 @@ def test_step_rejects_bad_geometry(bad, code):
     assert lib.g2k_last_error()
 
 
-def test_step_rejects_null_and_needs_no_workspace():
+def _split(x):
+    return x << _lib.STEP_SPLIT_SHIFT
+
+
+def test_step_rejects_null_and_sizes_the_split_workspace():
     lib = _lib.load()
     w = _lib.G2KWeights(*([ctypes.c_void_p(16)] * 7))
     p = ctypes.c_void_p(16)
     rc = lib.g2k_step_fused_f32(ctypes.byref(_dims()), ctypes.byref(w), None, p, p, p, p, None,
                                 None, p, p, p, p, None, None, 5e-4, p, 1 << 30, None)
     assert rc == -1
-    # every intermediate of the fused step stays on chip
-    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims())) == 0
+    # one workgroup per scene (S >= 256 CUs, or G2K_STEP_SPLIT(1)): every
+    # intermediate stays on chip
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims(S=256))) == 0
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims(flags=_split(1)))) == 0
+    # split scenes: one 64-byte ticket line per 16 scenes + [S][X][8] partials
+    # (S = 2: automatic X = min(4, 256 / S) = 4; S = 128: X = 2)
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims())) == 64 + 2 * 4 * 8 * 4
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims(S=128))) == 8 * 64 + 128 * 2 * 8 * 4
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims(flags=_split(2)))) == 64 + 2 * 2 * 8 * 4
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims(F=1))) == 0     # one frame: X = 1
     assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims(T=9))) == -1
     assert 0 < lib.g2k_step_lds_bytes(ctypes.byref(_dims())) <= 160 * 1024
+    # the split must name 0..4 workgroups, and X > 1 needs its workspace
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(_dims(flags=_split(5)))) == -1
+    rc = lib.g2k_step_fused_f32(ctypes.byref(_dims(flags=_split(5))), ctypes.byref(w), p, p, p, p,
+                                p, None, None, p, p, p, p, None, None, 5e-4, p, 1 << 30, None)
+    assert rc == -1
+    rc = lib.g2k_step_fused_f32(ctypes.byref(_dims()), ctypes.byref(w), p, p, p, p, p, None,
+                                None, p, p, p, p, None, None, 5e-4, None, 0, None)
+    assert rc == -1 and b"workspace" in lib.g2k_last_error()
 
 
 def test_other_entry_points_validate():
@@ -95,9 +115,12 @@ def test_gridlstm_and_train_entry_points_validate():
     d = _dims()
     assert lib.g2k_grad_size(ctypes.byref(d)) == 24 * 32 + 496
     need = lib.g2k_grad_workspace_bytes(ctypes.byref(d))
-    # one gradient row [P + 2] per scene (the fused kernel's output), then
-    # the 64-byte line of the folded update's ticket
-    assert need == 2 * (24 * 32 + 498) * 4 + 64
+    # one gradient row [P + 2] per workgroup (S X of them, the fused kernel's
+    # output), the 64-byte line of the folded update's ticket, then the split
+    # workspace (scene tickets, metric partials)
+    assert need == 2 * 4 * (24 * 32 + 498) * 4 + 64 + 64 + 2 * 4 * 8 * 4
+    one = lib.g2k_grad_workspace_bytes(ctypes.byref(_dims(flags=_split(1))))
+    assert one == 2 * (24 * 32 + 498) * 4 + 64
     assert lib.g2k_train_workspace_bytes(ctypes.byref(d)) == need
     w = _lib.G2KWeights(*([p] * 7))
     rc = lib.g2k_step_grad_f32(ctypes.byref(d), ctypes.byref(w), p, p, p, p, p, None, None, 5e-4,
