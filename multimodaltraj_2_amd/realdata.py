@@ -86,18 +86,43 @@ class SceneSource:
             have, self._plan = 0, None
         if count > have:
             new = self.loader.index.sample_scenes(self.pointers[have:count], nmax_cap)
-            new["content"] = _row_keys(self.canon[new["pos_col"]], self.canon[new["tgt_col"]])
+            w = max(1, int(new["n_nodes"].max(initial=0)))       # slots >= P are empty (-1)
+            new["content"] = _row_keys(self.canon[new["pos_col"][:, :, :w]],
+                                       self.canon[new["tgt_col"][:, :w]])
             self._plan = new if self._plan is None else {
                 k: np.concatenate([self._plan[k], new[k]]) for k in new}
             self._cap = nmax_cap
         return {k: v[:count] for k, v in self._plan.items()}
 
 
+_HASH = np.random.default_rng(0x9e3779b9).integers(1, 1 << 63, (2, 8 * 256 + 256 * 12),
+                                                     dtype=np.uint64) | np.uint64(1)
+
+
 def _row_keys(pos_col, tgt_col):
-    """One opaque (void) value per plan row: equal rows, equal values."""
-    rows = np.ascontiguousarray(np.concatenate(
-        [pos_col.reshape(len(pos_col), -1), tgt_col.reshape(len(tgt_col), -1)], axis=1))
-    return rows.view(np.dtype((np.void, rows.shape[1] * rows.itemsize))).reshape(-1)
+    """One 64-bit key per plan row (pos_col [n, 8, w], tgt_col [n, w, 12] of
+    canonical column ids, -1 = empty, any w >= the rows' P): equal rows, equal
+    keys.  A
+    multiply-add hash of (id + 1) per slot with a fixed multiplier per slot
+    (t, n) / (n, k), so the empty slots add nothing and the key does not
+    depend on how many slots are looked at; rows that share a key and differ
+    (never seen) fall back to exact keys by value."""
+    n, _, w = pos_col.shape
+    pc = (pos_col[:, :, :w].astype(np.int64) + 1).view(np.uint64)
+    tc = (tgt_col[:, :w, :].astype(np.int64) + 1).view(np.uint64)
+    mp = _HASH[0, :8 * 256].reshape(8, 256)[:, :w]
+    mt = _HASH[1, :256 * 12].reshape(256, 12)[:w]
+    with np.errstate(over="ignore"):
+        key = ((pc * mp).sum(axis=(1, 2), dtype=np.uint64)
+               + (tc * mt).sum(axis=(1, 2), dtype=np.uint64))
+    u, first, inv = np.unique(key, return_index=True, return_inverse=True)
+    if len(u) < len(key):                      # equal keys: equal rows?
+        f = first[inv.reshape(-1)]
+        if not (np.all(pc == pc[f], axis=(1, 2)) & np.all(tc == tc[f], axis=(1, 2))).all():
+            rows = np.concatenate([pc.reshape(n, -1), tc.reshape(n, -1)], axis=1)
+            _, key = np.unique(rows, axis=0, return_inverse=True)
+            key = key.reshape(-1).astype(np.uint64) | np.uint64(1 << 63)
+    return key
 
 
 @dataclass
