@@ -241,7 +241,7 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
                                                    const float (&rm)[4], float lam, float* as_dst,
                                                    int* as_flag, int flag_val, float* A_g,
                                                    float* cost_g, float* cost_l, int L, int q,
-                                                   bool want_m = true) {
+                                                   bool want_m = true, bool want_as = true) {
   // every operand load is unconditional (clamped addresses) and issued
   // before the first MFMA; the lanes' selects follow (an exec-masked load
   // would cost its own LDS round trip on the chain)
@@ -279,24 +279,26 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
   ua[2] = q < 2 ? ua[2] : (q == 2 ? ub : 0.f);
   va[2] = q == 3 ? 0.f : va[2];
   // the recurrence's operand first: E -> A -> As, the As flag; M (only the
-  // prediction tiles need it) after, so its six MFMAs do not hold up As
-  f32x4 eN = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);          // E[4q+i][L]
+  // prediction tiles need it) after, so its six MFMAs do not hold up As.
+  // (want_as false: the frame's As comes from a recurrence wave; want_m
+  // false: only As — wave-uniform)
   f32x4 aA = {0.f, 0.f, 0.f, 0.f};
-  {
+  if (want_as) {
+    f32x4 eN = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);          // E[4q+i][L]
     float em[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) em[i] = eN[i] * rm[i];                    // rm = 0 for t >= 8
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
       aA = mfma4(q < 2 ? lam * gA[ks] : 0.f, em[ks], aA);                 // A[4q+i][L]
+    __builtin_amdgcn_sched_barrier(0);
+    attn_weights(aA, as_dst, L, q);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // As stored before its flag
+    if ((threadIdx.x & 63) == 0) lds_store_flag(as_flag, flag_val);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  __builtin_amdgcn_sched_barrier(0);
-  attn_weights(aA, as_dst, L, q);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // As stored before its flag
-  if ((threadIdx.x & 63) == 0) lds_store_flag(as_flag, flag_val);
-  __builtin_amdgcn_sched_barrier(0);
   FrameHeadOut o;
   o.mT0 = f32x4{0.f, 0.f, 0.f, 0.f};
   o.mT1 = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -307,7 +309,7 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
       o.mT1 = mfma4(va[ks], by[ks], o.mT1);   // M[12+L][4q+i]    (y rows)
     }
   }
-  if (A_g) {
+  if (A_g && want_as) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) A_g[(4 * q + i) * kD + L] = aA[i];
   }
@@ -503,6 +505,27 @@ __device__ __forceinline__ void scene_nll_consts(const SceneCtx& c) {
   }
 }
 
+// Rm = Wr @ Rel, Rel = Ve * Ve (train.py:194-195, g2k_lstm_mcr.py:106):
+// rows t = 4q + i of column L, zero for t >= 8 (unconditional loads, rows t
+// of lane groups 2, 3 clamped, then selects)
+__device__ __forceinline__ void scene_rm(const SceneLayout& lay, const SceneCtx& c, float (&rm)[4]) {
+  const int L = c.L, q = c.q;
+  const float ve0 = c.sV[lay.wcmax * kD + L], ve1 = c.sV[(lay.wcmax + 1) * kD + L];
+  float2 wr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) wr[i] = *reinterpret_cast<const float2*>(c.sm + SM_WR + 2 * (4 * (q & 1) + i));
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    rm[i] = lane_sel(q < 2, fmaf(wr[i].x, ve0 * ve0, wr[i].y * (ve1 * ve1)), 0.f);
+}
+
+// Frames 0 .. n-1 whose As the recurrence waves form themselves (one frame
+// per wave, right after the first staging; the scene's recurrence workgroup)
+__device__ __forceinline__ int rec_head_frames(const SceneLayout& lay, const SceneCtx& c) {
+  const int n = c.nf < lay.fc ? c.nf : lay.fc;
+  return n < kRecW ? n : kRecW;
+}
+
 // Chunk staging shared by both roles (every wave takes part).  The chunk's
 // position window is in flight by LDS-DMA.  Wait, barrier; the producer
 // waves compute the embedding-row tiles (scene_vtile) and, at the first
@@ -559,6 +582,23 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     scene_stage<NT, NP>(a, lay, c, 0, c.nf < lay.fc ? c.nf : lay.fc, [&] {
       if (live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
     });
+  // the first frames' attention weights (E -> A -> As into the ring, the
+  // flag) by the recurrence waves themselves, one frame per wave at top
+  // priority: the producers reach their first heads only after their loop
+  // set-up (thousands of cycles of scalar work on the CU's one scalar unit);
+  // they form only M for these frames
+  if (live && c.wv < rec_head_frames(lay, c)) {
+    __builtin_amdgcn_s_setprio(3);
+    float rm[4];
+    scene_rm(lay, c, rm);
+    const int fl = c.wv;
+    const bool mine = c.X == 1 || fl % c.X == 0;
+    frame_head(c.sm, c.sV, c.sVG, fl * a.d.stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
+               c.sFlag + fl, fl + 1,
+               a.A_out && mine ? a.A_out + ((size_t)c.s * a.d.F + fl) * kD * kD : nullptr, nullptr,
+               nullptr, c.L, c.q, /*want_m=*/false);
+    __builtin_amdgcn_s_setprio(0);
+  }
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) {
@@ -1327,37 +1367,29 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       load_item(fb, nitems, 0, tgA);
       load_item(fb, nitems, 1, tgB);
     }
-    // Rm = Wr @ Rel, Rel = Ve * Ve (train.py:194-195, g2k_lstm_mcr.py:106):
-    // rows t = 4q + i of column L, zero for t >= 8
     float rm[4];
-    {
-      // unconditional loads (rows t of lane groups 2, 3 clamped), then selects
-      const float ve0 = c.sV[lay.wcmax * kD + L], ve1 = c.sV[(lay.wcmax + 1) * kD + L];
-      float2 wr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) wr[i] = *reinterpret_cast<const float2*>(c.sm + SM_WR + 2 * (4 * (q & 1) + i));
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        rm[i] = lane_sel(q < 2, fmaf(wr[i].x, ve0 * ve0, wr[i].y * (ve1 * ve1)), 0.f);
-    }
+    scene_rm(lay, c, rm);
     // phase 1 — the critical path: frame heads in frame order, As and M into
     // the rings, then the frame's flags; the first heads the recurrence will
     // wait for get the issue priority.  The workgroup running the recurrence
     // forms every frame's head (As), the others only their own frames'; M
-    // (and A / cost out) only for own frames.
+    // (and A / cost out) only for own frames.  The recurrence waves form As
+    // of the first chunk's frames 0 .. nrh - 1 themselves (M only here).
     const bool all_heads = a.h_in != nullptr && c.x == 0;
     const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : c.X, nh = all_heads ? cnt : own.n;
+    const int nrh = all_heads && fb == 0 ? rec_head_frames(lay, c) : 0;
     for (int i = pw; i < nh; i += NP) {
       const int fl = hb + hs * i;
       const int f = fb + fl;
       const bool mine = !all_heads || c.X == 1 || f % c.X == c.x;
-      if (fl < kRecW) __builtin_amdgcn_s_setprio(1);
+      if (fl < nrh && !mine) continue;                   // (neither As nor M wanted here)
+      if (fl >= nrh && fl < kRecW + nrh) __builtin_amdgcn_s_setprio(1);
       const FrameHeadOut hd =
           frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                      c.sFlag + fl, f + 1,
                      a.A_out && mine ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
                      a.cost_out && mine ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr,
-                     GRAD ? c.sCost + fl * kT * kT : nullptr, L, q, mine);
+                     GRAD ? c.sCost + fl * kT * kT : nullptr, L, q, mine, fl >= nrh);
       if (mine) {
         if (L < kL && q < 2) {
           float* m = c.sMring + fl * kL2 * kT;

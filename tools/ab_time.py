@@ -96,8 +96,9 @@ TL_FWD = [
      "  G2K_ST(4, " + P0 + " && fb == 0);\n  __builtin_amdgcn_s_barrier();\n  G2K_ST(5, " + P0 + " && fb == 0);"),
     ("  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2",
      "  G2K_ST(51, " + P0 + " && fb == 0);\n  __builtin_amdgcn_s_barrier();\n  G2K_ST(6, " + P0 + " && fb == 0);"),
-    ("      const FrameHeadOut hd =", "      G2K_ST(7 + 2 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n      const FrameHeadOut hd ="),
-    ("      if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n", "      if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      G2K_ST(8 + 2 * (fl / NP), " + P0 + " && fb == 0 && fl < 3 * NP);\n"),
+    ("      const FrameHeadOut hd =", "      G2K_ST(7 + 2 * (i / NP), " + P0 + " && fb == 0 && i < 3 * NP);\n      const FrameHeadOut hd ="),
+    ("        if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      }\n",
+     "        if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      }\n      G2K_ST(8 + 2 * (i / NP), " + P0 + " && fb == 0 && i < 3 * NP);\n"),
     ("        poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)",
      "        G2K_ST(13 + 2 * k, " + P0 + " && k < 6);\n        poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)\n        G2K_ST(14 + 2 * k, " + P0 + " && k < 6);"),
     ("  publish_metrics(a, c, pw, GRAD ? NP + kRecW : NP, acc, lsum, GRAD);",
@@ -132,7 +133,7 @@ __shared__ unsigned g2k_lds_stamp[160];
 #define G2K_ST(k, cond) do { if ((cond) && (threadIdx.x & 63) == 0) { \\
   g2k_lds_stamp[(k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
 """
-HEAD_ST = "__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 4 && wrow0 == 0"
+HEAD_ST = "wrow0 == 0"
 
 
 def lds_stamps(reps, head=True):
@@ -149,14 +150,27 @@ def lds_stamps(reps, head=True):
     ]
     if head:
         out += [
-        ("  f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);",
-         "  G2K_ST(60, " + HEAD_ST + ");\n  f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n  for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);"),
-        ("  __builtin_amdgcn_sched_barrier(0);\n  attn_weights(aA, as_dst, L, q);",
-         "  G2K_ST(61, " + HEAD_ST + " && aA[0] != 12345.f);\n  __builtin_amdgcn_sched_barrier(0);\n  attn_weights(aA, as_dst, L, q);"),
+        ("    f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n    for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);",
+         "    G2K_ST(60, " + HEAD_ST + ");\n    f32x4 eN = {0.f, 0.f, 0.f, 0.f};\n#pragma unroll\n    for (int ks = 0; ks < 3; ++ks) eN = mfma4(ka[ks], ua[ks], eN);"),
+        ("    __builtin_amdgcn_sched_barrier(0);\n    attn_weights(aA, as_dst, L, q);",
+         "    G2K_ST(61, " + HEAD_ST + " && aA[0] != 12345.f);\n    __builtin_amdgcn_sched_barrier(0);\n    attn_weights(aA, as_dst, L, q);"),
         ("  if ((threadIdx.x & 63) == 0) lds_store_flag(as_flag, flag_val);",
          "  if ((threadIdx.x & 63) == 0) lds_store_flag(as_flag, flag_val);\n  G2K_ST(62, " + HEAD_ST + ");"),
     ]
     return out
+
+
+# the producers' lead-in between the staging barrier and the first head
+TL_GAP = [
+    ("    if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)",
+     "    G2K_ST(70, " + P0 + " && fb == 0);\n    if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)\n    G2K_ST(71, " + P0 + " && fb == 0);"),
+    ("    float rm[4];\n    scene_rm(lay, c, rm);\n    // phase 1",
+     "    G2K_ST(72, " + P0 + " && fb == 0);\n    float rm[4];\n    scene_rm(lay, c, rm);\n    // phase 1"),
+    ("    if (fb == 0 && live) {\n      // softmax(h) numerators",
+     "    G2K_ST(74, " + R0 + " && fb == 0);\n    if (fb == 0 && live) {\n      // softmax(h) numerators"),
+    ("    if (live) {\n      __builtin_amdgcn_s_setprio(2);",
+     "    G2K_ST(75, " + R0 + " && fb == 0);\n    if (live) {\n      __builtin_amdgcn_s_setprio(2);"),
+]
 
 
 # I-cache experiment: every producer runs the staging and frame-head code once
@@ -304,6 +318,7 @@ VARIANTS = {
     "tl_fwd": {SCENE: TL_FWD},
     "tl_rec": {SCENE: TL_REC},
     "tl_lds": {SCENE: lds_stamps(TL_REC)},
+    "tl_gap": {SCENE: lds_stamps(TL_REC + TL_GAP)},
     "tl_tile": {SCENE: lds_stamps(TL_REC + TL_TILE)},
     "tl_b1": {SCENE: lds_stamps(TL_B1 + TL_REC)},
     "pos1k": {SCENE: POS1K},
@@ -527,13 +542,13 @@ def main():
                 for _ in range(5):
                     plan.run()
             torch.cuda.synchronize()
-            W = 160 if name in ("tl_lds", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig") else 64
+            W = 160 if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig") else 64
             buf = (ctypes.c_uint * (S * W))()
             assert lib.g2k_stamp_copy(buf, S * W) == 0
             st = np.frombuffer(buf, dtype=np.uint32).reshape(S, W).astype(np.int64)
             {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print, "tl_end_orig": tl_end_print}.get(name, tl_rec_print)(st, t)
             print(f"{name}: fwd {time_it(plan.run):7.2f} us (stamped build)")
-            if name in ("tl_lds", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k"):
+            if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k"):
                 rel = (st - st[:, :1]) % (1 << 32)
                 med = np.median(rel, axis=0)
                 print("head 0 (median): operands", int(med[60]), "A done", int(med[61]), "attn done",
@@ -544,6 +559,11 @@ def main():
                     print("wave DMA issue start (median):", [int(med[96 + w]) for w in range(16)])
                     print("wave nact loaded (median):", [int(med[112 + w]) for w in range(16)])
                     print("wave at staging, before its DMA wait (median):", [int(med[128 + w]) for w in range(16)])
+                if name == "tl_gap":
+                    print("P0 lead-in (median): B2", int(med[6]), "mask", int(med[70]), int(med[71]),
+                          "targets issued", int(med[72]), "first head", int(med[7]), int(med[8]),
+                          "second head", int(med[9]), int(med[10]),
+                          "| R0 at init", int(med[74]), "R0 init done", int(med[75]))
                 if name == "tl_tile":
                     print("last tile (median): entry", int(med[40]), "Y", int(med[41]), "targets", int(med[42]),
                           "stores", int(med[43]), "errors", int(med[44]))
