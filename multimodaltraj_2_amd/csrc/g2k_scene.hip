@@ -562,12 +562,12 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
   __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2
 }
 
-// Role 1: the recurrence (waves 0..3).  Without h_in (gradient only) the
-// waves only take part in the chunk barriers.  h is loaded during the first
-// staging (after B1: the prologue's HBM burst, which every wave's B1 waits
-// for, stays free of it) and its softmax numerators are formed after B2,
-// while the producers compute the first frame heads the chain waits for
-// anyway.
+// Role 1: the recurrence (waves 0..3).  Without h_in (gradient only, or a
+// split scene's other workgroups) the waves only take part in the chunk
+// barriers.  h is loaded during the first staging (after B1: the prologue's
+// HBM burst, which every wave's B1 waits for, stays free of it) and its
+// softmax numerators are formed there too; after B2 the waves form As of the
+// first frames themselves and start the chain.
 template <int TPW, int NP>
 __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneLayout& lay,
                                                  const SceneCtx& c) {
@@ -577,10 +577,22 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   const bool live = a.h_in != nullptr && c.x == 0;   // (the scene's first workgroup)
   RecurH<TPW, kRecW> rc;
   int* seq = reinterpret_cast<int*>(c.sRed + 2 * kRB);   // 2 partial buffers, seq words, row max
-  // the first chunk's staging ahead of the chunk loop (see scene_producer)
+  // the first chunk's staging ahead of the chunk loop (see scene_producer);
+  // the recurrence waves load h and form its softmax numerators meanwhile
+  // (row max exchange: seq 1; e and its row partials into buffer 0: seq 2),
+  // off the chain's critical path, which starts with the first heads after
+  // the staging
   if (c.nf > 0)
     scene_stage<NT, NP>(a, lay, c, 0, c.nf < lay.fc ? c.nf : lay.fc, [&] {
-      if (live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
+      if (!live) return;
+      rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
+      rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
+      asm volatile("" ::: "memory");
+      if (c.lane == 0) lds_store_flag(seq + c.wv, 1);
+      poll_seq(seq + (c.L & 3), 1);
+      rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
+      asm volatile("" ::: "memory");
+      if (c.lane == 0) lds_store_flag(seq + c.wv, 2);
     });
   // the first frames' attention weights (E -> A -> As into the ring, the
   // flag) by the recurrence waves themselves, one frame per wave at top
@@ -604,17 +616,6 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     if (fb > 0) {
       scene_pos_dma<NT>(a, lay, c, fb, cnt);
       scene_stage<NT, NP>(a, lay, c, fb, cnt, [] {});
-    }
-    if (fb == 0 && live) {
-      // softmax(h) numerators: row max exchange (seq 1), then e and its row
-      // partials into buffer 0 (seq 2), no workgroup barrier
-      rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
-      asm volatile("" ::: "memory");
-      if (c.lane == 0) lds_store_flag(seq + c.wv, 1);
-      poll_seq(seq + (c.L & 3), 1);
-      rc.init_exp(c.sRed, c.sRed + 3 * kRB, c.wv, c.q, c.L);
-      asm volatile("" ::: "memory");
-      if (c.lane == 0) lds_store_flag(seq + c.wv, 2);
     }
     if (live) {
       __builtin_amdgcn_s_setprio(2);

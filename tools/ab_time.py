@@ -232,20 +232,32 @@ POS1K = [
 TL_END = [
     ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk", "namespace g2k {\n" + STAMP_DEF + "namespace {\n\nconstexpr int kSceneChunk"),
     ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
-     "  G2K_ST(0, c.tid == 0);\n  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+     "  G2K_ST(0, c.tid == 0);\n  if (c.tid == 0) g2k_stamp_buf[(size_t)c.s * 64 + 27] = (unsigned)__builtin_amdgcn_s_memrealtime();\n"
+     "  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
     ('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup',
-     '  G2K_ST(64 + c.wv, true);\n  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup'),
+     '  G2K_ST(64 + c.wv, true);\n  if (c.lane == 0) g2k_stamp_buf[(size_t)c.s * 64 + 28] = (unsigned)__builtin_amdgcn_s_memrealtime();\n'
+     '  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup'),
 ]
 
 
 def tl_end_print(st, t):
     import numpy as np
+    rt = st[:, 27:29].copy()
     rel = (st - st[:, :1]) % (1 << 32)
-    print("WG duration (wave 0 start -> last wave exit, cycles): median", int(np.median(rel[:, 64:76].max(1))),
-          "max", int(rel[:, 64:76].max()))
-    ends = rel[:, 64:76]
+    rel[:, 27:29] = 0
+    span = (rt[:, 1] - rt[:, 0]) % (1 << 32)         # 100 MHz ticks, wave 0 start -> a late wave's exit
+    cyc = rel[:, 64:80].max(1)
+    ok = span > 0
+    if ok.any():
+        print("in-kernel clock (cycles / realtime, median over WGs): %.3f GHz; WG start spread %d ticks, "
+              "last WG end - first WG start %d ticks" % (float(np.median(cyc[ok] / (span[ok] * 10.0))),
+                                                      int(rt[:, 0].max() - rt[:, 0].min()),
+                                                      int(rt[:, 1].max() - rt[:, 0].min())))
+    print("WG duration (wave 0 start -> last wave exit, cycles): median", int(np.median(rel[:, 64:80].max(1))),
+          "max", int(rel[:, 64:80].max()))
+    ends = rel[:, 64:80]
     na = t["n_active"].cpu().numpy()
-    print("wave exits (median over scenes, waves 0..11):", [int(x) for x in np.median(ends, axis=0)])
+    print("wave exits (median over scenes, waves 0..15):", [int(x) for x in np.median(ends, axis=0)])
     for lo, hi in ((0, 8), (8, 16), (16, 24), (24, 33)):
         m = (na >= lo) & (na < hi)
         if m.any():
@@ -296,7 +308,10 @@ def tl_fwd_print(st, t):
     print("median items:", " ".join(f"({int(med[13 + 2 * k])},{int(med[14 + 2 * k])})" for k in range(6)))
 
 
-NO_RECUR = [("  const bool live = a.h_in != nullptr;", "  const bool live = false;")]
+NO_RECUR = [("  const bool live = a.h_in != nullptr && c.x == 0;   // (the scene's first workgroup)",
+             "  const bool live = false;")]
+NO_TILES = [("    const int nitems = own.n * ntact > pw ? (own.n * ntact - pw + NP - 1) / NP : 0;   // forward",
+             "    const int nitems = 0;")]
 NO_RECUR_SCENE = {SCENE: NO_RECUR}
 VARIANTS = {
     "base": {},
@@ -311,6 +326,13 @@ VARIANTS = {
     "stamps_norecur": {SCENE: STAMPS + NO_RECUR},
     "nolsr": {"__flags__": ["-mllvm", "-disable-lsr"]},
     "no_recur": NO_RECUR_SCENE,
+    "no_tiles": {SCENE: NO_TILES},
+    "rec8": {SCENE: [("constexpr int kRecHeads = kRecW;", "constexpr int kRecHeads = 2 * kRecW;")]},
+    "tl_end_rec8": {SCENE: lds_stamps(TL_END, head=False) + [("constexpr int kRecHeads = kRecW;", "constexpr int kRecHeads = 2 * kRecW;")]},
+    "no_tile_mfma": {SCENE: [("      y0 = mfma4(a0[ks], w, y0);                           // Y[4q + v][n]\n      y1 = mfma4(L < kT ? a1[ks] : 0.f, w, y1);            // Y[16 + 4q + v][n] (0 for q >= 2)",
+                              "      y0[0] = fmaf(a0[ks], w, y0[0]);\n      y1[0] = fmaf(a1[ks], w, y1[0]);")]},
+    "no_m_mfma": {SCENE: [("      o.mT0 = mfma4(va[ks], bx[ks], o.mT0);   // M[L][4q+i]       (x rows)\n      o.mT1 = mfma4(va[ks], by[ks], o.mT1);   // M[12+L][4q+i]    (y rows)",
+                           "      o.mT0[0] = fmaf(va[ks], bx[ks], o.mT0[0]);\n      o.mT1[0] = fmaf(va[ks], by[ks], o.mT1[0]);")]},
     "no_pred_store": {SCENE: [("      bstore(pr, n < nact ? (mrow(4 * q + v) * Nmax + n) * 4 : kBufOff, y0[v]);\n      bstore(pr, (n < nact && hi) ? (mrow(16 + 4 * q + v) * Nmax + n) * 4 : kBufOff, y1[v]);", "")]},
     "stamps_nolsr": {SCENE: STAMPS, "__flags__": ["-mllvm", "-disable-lsr"]},
     "stamps_tile": {SCENE: STAMPS + TILE},
@@ -542,11 +564,11 @@ def main():
                 for _ in range(5):
                     plan.run()
             torch.cuda.synchronize()
-            W = 160 if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig") else 64
+            W = 160 if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig", "tl_end_rec8") else 64
             buf = (ctypes.c_uint * (S * W))()
             assert lib.g2k_stamp_copy(buf, S * W) == 0
             st = np.frombuffer(buf, dtype=np.uint32).reshape(S, W).astype(np.int64)
-            {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print, "tl_end_orig": tl_end_print}.get(name, tl_rec_print)(st, t)
+            {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print, "tl_end_orig": tl_end_print, "tl_end_rec8": tl_end_print}.get(name, tl_rec_print)(st, t)
             print(f"{name}: fwd {time_it(plan.run):7.2f} us (stamped build)")
             if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k"):
                 rel = (st - st[:, :1]) % (1 << 32)

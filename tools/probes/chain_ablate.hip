@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(256) chain(unsigned long long* out, float* hou
         z[i] = t;
       }
       a0 = b.x * rcp(z[0]); a1 = b.y * rcp(z[1]); a2 = b.z * rcp(z[2]); a3 = b.w * rcp(z[3]);
-      split4<0, 4>(A, a0, a1, a2, a3);
+      A = __builtin_bit_cast(f16x8, split4(a0, a1, a2, a3));
     }
     __builtin_amdgcn_sched_barrier(0);
     f32x4 acc[TPW];
@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(256) chain(unsigned long long* out, float* hou
     if (!(OFF & NO_SPLIT)) {
 #pragma unroll
       for (int t = 0; t < TPW; ++t) {
-        split4<0, 4>(bo[t], e[t][0], e[t][1], e[t][2], e[t][3]);
+        bo[t] = __builtin_bit_cast(f16x8, split4(e[t][0], e[t][1], e[t][2], e[t][3]));
 #pragma unroll
         for (int j = 0; j < 4; ++j) { bs[t][j] = bo[t][4 + j]; bs[t][4 + j] = bo[t][j]; }
       }
