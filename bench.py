@@ -227,6 +227,62 @@ def event_time(step, reps, stream):
     return ev0.elapsed_time(ev1) / 1e3 / reps
 
 
+class GraphSteps:
+    """Steps replayed from a HIP graph (torch.cuda.CUDAGraph over the plans'
+    stream): ``n`` consecutive calls of ``step(i0 + i)`` captured once, then
+    one graph launch runs all of them back to back on the GPU — the host's
+    per-launch cost (Python, the C ABI's checks, hipLaunchKernel) no longer
+    paces a ~20 us step.  ``run(i)`` with i a multiple of ``n`` replays it."""
+
+    def __init__(self, step, n, stream, i0=0):
+        self.n = n
+        self.g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(self.g, stream=stream):
+            for i in range(n):
+                step(i0 + i)
+        torch.cuda.synchronize()
+
+    def replay(self):
+        self.g.replay()
+
+
+def timed_graph(step, n, warmup, dist, sync, stream):
+    """timed() with the warm-up and the timed steps each as one graph replay
+    (exactly ``n`` steps between the barriers)."""
+    gw = GraphSteps(step, max(warmup, 1), stream)
+    gm = GraphSteps(step, n, stream, i0=max(warmup, 1))
+    gw.replay()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    gm.replay()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        e = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    return el, gm
+
+
+def graph_event_time(g, stream):
+    """Average seconds per step of a captured graph's replay (HIP events on its stream)."""
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    g.replay()
+    ev0.record(stream)
+    g.replay()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / 1e3 / g.n
+
+
 def load_pmc(name):
     p = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
     if not os.path.exists(p):
@@ -304,6 +360,9 @@ def main(argv=None):
     ap.add_argument("--split", type=int, default=0,
                     help="workgroups per scene (G2K_STEP_SPLIT; 0: automatic, enough to cover "
                          "the CUs when a rank has fewer scenes than CUs)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch every step from the host instead of replaying the timed steps "
+                         "from a HIP graph")
     ap.add_argument("--selftest-launcher", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 
@@ -347,6 +406,7 @@ def main(argv=None):
     params = params_host.to(dev)
     pbytes = sum(getattr(params, k).numel() * 4 for k in ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo"))
     shared = args.config == REAL          # real scenes: one target set per scene (every frame's)
+    stream = torch.cuda.Stream(device=dev)   # the plans' stream (graph capture needs a non-default one)
     layout = dict(pred_layout=args.pred_layout, targets_shared=shared, frames=F if shared else None,
                   split=args.split)
     abytes = algorithmic_bytes(b, H, pbytes, shared)
@@ -371,24 +431,31 @@ def main(argv=None):
         batches.append(t)
         plans.append(fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"],
                                  t["n_active"], t["h0"], n_frames=t["n_frames"],
-                                 ped_mask=t["ped_mask"], stride=b.stride, out=out, **layout))
+                                 ped_mask=t["ped_mask"], stride=b.stride, out=out, stream=stream,
+                                 **layout))
 
     def step(i):
         plans[i % K].run()
 
-    elapsed = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    if args.no_graph:
+        elapsed = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    else:
+        elapsed, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream)
     # reference mode: replicas only; the ADE/FDE numerators of the last batch
     # are summed across ranks once at the end
     tot = plans[(args.steps - 1) % K].out.metrics.double().sum(dim=0)
     if dist is not None:
         dist.all_reduce(tot)
-    stream = torch.cuda.current_stream()
-    kern_s = event_time(step, max(20, min(args.steps, 200)), stream)
+    if args.no_graph:
+        kern_s = event_time(step, max(20, min(args.steps, 200)), stream)
+    else:
+        kern_s = graph_event_time(gm, stream)
     achieved = abytes / kern_s / 1e9
 
     train = None
     if not args.no_train:
-        train = time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, layout)
+        train = time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, layout,
+                           stream)
 
     if rank == 0:
         m = tot.cpu().numpy()
@@ -415,7 +482,9 @@ def main(argv=None):
                        "frames_per_step": b.frames, "obs_len": 8, "pred_len": 12, "Nmax": Nmax,
                        "hidden": H, "D": 16, "parallelism": f"dp{world}",
                        "input_batches_rotated": K, "pred_layout": args.pred_layout,
-                       "targets_shared": shared, "workgroups_per_scene": split_of(S, F, args.split)},
+                       "targets_shared": shared, "workgroups_per_scene": split_of(S, F, args.split),
+                       "launch": "host launch per step" if args.no_graph else
+                                 "HIP graph of the timed steps (one replay)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": load_pmc(args.config),
@@ -443,7 +512,7 @@ def split_of(S, F, requested):
     return max(1, min(x, 4, max(F, 1)))
 
 
-def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, layout):
+def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, layout, stream):
     """--mode train: the same step plus loss gradient, ONE
     all-reduce of the flat [P + 2] gradient buffer across ranks (RCCL under
     the nccl backend) and the RMSProp update (multimodaltraj_2_amd/train_step.py).
@@ -454,7 +523,7 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
         params.head = torch.zeros((3, 12), device=dev)
     ts = TrainStep(params, t0["pos"], t0["vislet"], t0["G"], t0["targets"], t0["n_active"],
                    t0["h0"], n_frames=t0["n_frames"], ped_mask=t0["ped_mask"], stride=b.stride,
-                   loss=args.loss, **layout)
+                   loss=args.loss, stream=stream if world == 1 else None, **layout)
     for t in batches[1:]:
         ts.bind(t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
                 n_frames=t["n_frames"], ped_mask=t["ped_mask"])
@@ -463,9 +532,17 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
     def step(i):
         last["g"] = ts.run(i % K)
 
-    el = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    # one rank: one C call per step (gradient + update), replayed from a HIP
+    # graph; across ranks the all-reduce sits between two launches (eager)
+    graph = not args.no_graph and world == 1
+    if graph:
+        el, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream)
+        kern_s = graph_event_time(gm, stream)
+    else:
+        el = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+        st = stream if world == 1 else torch.cuda.current_stream()
+        kern_s = event_time(step, max(20, min(args.steps, 200)), st)
     gl = last["g"].double().cpu().numpy()
-    kern_s = event_time(step, max(20, min(args.steps, 200)), torch.cuda.current_stream())
     abytes = train_algorithmic_bytes(b, H, pbytes, ts.P, layout["targets_shared"])
     achieved = abytes / kern_s / 1e9
     return {"metric": f"frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + "

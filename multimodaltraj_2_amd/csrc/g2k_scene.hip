@@ -1109,14 +1109,16 @@ __device__ __forceinline__ unsigned scene_act_bits(const SceneCtx& c, uint32_t w
   for (int b = 0; b < 4; ++b) B[b] = __builtin_amdgcn_ballot_w64(((w >> (8 * b)) & 0xffu) != 0);
   const int b = c.L & 3;
   const unsigned long long mine = b == 0 ? B[0] : b == 1 ? B[1] : b == 2 ? B[2] : B[3];
-  unsigned bits = 0;
-#pragma unroll
-  for (int t = 0; t < kMaxN / 16; ++t) {
-    const int n = 16 * t + c.L;
-    const unsigned on = (unsigned)((mine >> (4 * t + (c.L >> 2))) & 1ull);
-    bits |= (n < c.nact ? on : 0u) << t;
-  }
-  return bits;
+  // bits 4 t + L / 4 of `mine` (t = 0..15) gathered into bits t: a
+  // shift-and-mask compression instead of one 64-bit shift per tile
+  unsigned long long x = (mine >> (c.L >> 2)) & 0x1111111111111111ull;
+  x = (x | (x >> 3)) & 0x0303030303030303ull;
+  x = (x | (x >> 6)) & 0x000F000F000F000Full;
+  x = (x | (x >> 12)) & 0x000000FF000000FFull;
+  x = (x | (x >> 24)) & 0xFFFFull;
+  // and only tiles t with 16 t + L < n_active
+  const int nt = c.nact > c.L ? (c.nact - c.L + 15) >> 4 : 0;
+  return (unsigned)x & ((1u << nt) - 1u);
 }
 
 // Train mode: the last R frames of the scene's last chunk go to the

@@ -90,37 +90,39 @@ __device__ __forceinline__ void update_body(float* __restrict__ params, float* _
   }
 }
 
-// grad[p] = sum_s rows[s][p]: workgroup = 64 columns x 16 row slices; slice
-// k sums rows k, k + 16, ... in order (eight loads in flight), then the 16
-// slices in order (the same sum for every launch: deterministic, no atomics
-// on data).  UPD: the workgroup that finishes last then runs the optimizer
-// step on the complete gradient (one launch fewer per train step).  The
-// hand-off uses agent-scope atomics only — gradient stores that write
+// grad[p] = sum_s rows[s][p]: workgroup = 32 columns x 32 row slices; slice
+// k sums rows k, k + 32, ... in order with eight loads in flight (the rows
+// one thread adds — 8 of the usual 256 — come in ONE memory round trip),
+// then the 32 slices in order (the same sum for every launch: deterministic,
+// no atomics on data).  UPD: the workgroup that finishes last then runs the
+// optimizer step on the complete gradient (one launch fewer per train step).
+// The hand-off uses agent-scope atomics only — gradient stores that write
 // through to the coherence point (sc1), their completion (vmcnt(0)) before
 // the ticket's fetch-add, coherent loads by the last workgroup — so no L2
 // write-back / invalidate is needed (a __threadfence() here costs a full L2
 // write-back and invalidate per workgroup: measured +8 us per step).
-constexpr int kRowSlices = 16;
+constexpr int kRowSlices = 32, kRowCols = 32;
 template <bool UPD>
-__global__ void __launch_bounds__(64 * kRowSlices) g2k_grad_rows_kernel(const float* __restrict__ rows,
-                                                                        int S, int width,
-                                                                        float* __restrict__ grad,
-                                                                        UpdateArgs up) {
-  __shared__ float red[kRowSlices][64];
+__global__ void __launch_bounds__(kRowCols * kRowSlices) g2k_grad_rows_kernel(const float* __restrict__ rows,
+                                                                              int S, int width,
+                                                                              float* __restrict__ grad,
+                                                                              UpdateArgs up) {
+  __shared__ float red[kRowSlices][kRowCols + 1];
   __shared__ int last;
-  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int p = blockIdx.x * 64 + c;
+  const int c = threadIdx.x % kRowCols, sl = threadIdx.x / kRowCols;
+  const int p = blockIdx.x * kRowCols + c;
   float acc = 0.f;
   if (p < width) {
-    int r = sl;
-    for (; r + 7 * kRowSlices < S; r += 8 * kRowSlices) {
+    for (int r0 = sl; r0 < S; r0 += 8 * kRowSlices) {
       float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = rows[(size_t)(r + i * kRowSlices) * width + p];
+      for (int i = 0; i < 8; ++i) {
+        const int r = r0 + i * kRowSlices;
+        v[i] = rows[(size_t)(r < S ? r : S - 1) * width + p];
+      }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc += v[i];
+      for (int i = 0; i < 8; ++i) acc += r0 + i * kRowSlices < S ? v[i] : 0.f;
     }
-    for (; r < S; r += kRowSlices) acc += rows[(size_t)r * width + p];
   }
   red[sl][c] = acc;
   __syncthreads();
@@ -159,7 +161,7 @@ __global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ pa
 
 int grad_rows_launch(const float* rows, int S, int width, float* grad, hipStream_t st,
                      const UpdateArgs* up) {
-  const dim3 grid((width + 63) / 64), block(64 * kRowSlices);
+  const dim3 grid((width + kRowCols - 1) / kRowCols), block(kRowCols * kRowSlices);
   if (up) {
     hipLaunchKernelGGL(g2k_grad_rows_kernel<true>, grid, block, 0, st, rows, S, width, grad, *up);
   } else {

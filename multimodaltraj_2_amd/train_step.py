@@ -217,9 +217,10 @@ class TrainStep:
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
                  lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,
                  n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None,
-                 pred_layout="band", targets_shared=False, frames=None, loss="l2", split=0):
+                 pred_layout="band", targets_shared=False, frames=None, loss="l2", split=0,
+                 stream=None):
         self._layout = dict(pred_layout=pred_layout, targets_shared=targets_shared, frames=frames,
-                            loss=loss, split=split)
+                            loss=loss, split=split, stream=stream)
         self.flat, self.params = flat_params(params, loss)
         self.P = self.flat.numel()
         self.ms = torch.ones_like(self.flat) if rmsprop else None

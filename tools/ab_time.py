@@ -313,6 +313,47 @@ NO_RECUR = [("  const bool live = a.h_in != nullptr && c.x == 0;   // (the scene
 NO_TILES = [("    const int nitems = own.n * ntact > pw ? (own.n * ntact - pw + NP - 1) / NP : 0;   // forward",
              "    const int nitems = 0;")]
 NO_RECUR_SCENE = {SCENE: NO_RECUR}
+# every producer's first head ahead of the chunk loop (and its set-up)
+PEEL = [
+    ("  for (int fb = 0; fb < c.nf; fb += lay.fc) {\n    const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;\n    if (fb > 0) {\n      scene_pos_dma<64 * (kRecW + NP)>",
+     "  int peeled = 0;\n"
+     "  if (c.nf > 0) {\n"
+     "    const int cnt = c.nf < lay.fc ? c.nf : lay.fc;\n"
+     "    const OwnFrames own = own_frames(0, cnt, c.X, c.x);\n"
+     "    const bool all_heads = a.h_in != nullptr && c.x == 0;\n"
+     "    const int nrh = all_heads ? rec_head_frames(lay, c) : 0;\n"
+     "    if (pw < (all_heads ? cnt : own.n)) {\n"
+     "      peeled = NP;\n"
+     "      const int fl = all_heads ? pw : own.fo + c.X * pw;\n"
+     "      const int f = fl;\n"
+     "      const bool mine = !all_heads || c.X == 1 || f % c.X == c.x;\n"
+     "      if (!(fl < nrh && !mine)) {\n"
+     "        float rm[4];\n"
+     "        scene_rm(lay, c, rm);\n"
+     "        if (fl >= nrh && fl < kRecW + nrh) __builtin_amdgcn_s_setprio(1);\n"
+     "        const FrameHeadOut hd =\n"
+     "            frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,\n"
+     "                       c.sFlag + fl, f + 1,\n"
+     "                       a.A_out && mine ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,\n"
+     "                       a.cost_out && mine ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr,\n"
+     "                       GRAD ? c.sCost + fl * kT * kT : nullptr, L, q, mine, fl >= nrh);\n"
+     "        if (mine) {\n"
+     "          if (L < kL && q < 2) {\n"
+     "            float* m = c.sMring + fl * kL2 * kT;\n"
+     "            *reinterpret_cast<float4*>(m + L * kT + 4 * q) = make_float4(hd.mT0[0], hd.mT0[1], hd.mT0[2], hd.mT0[3]);\n"
+     "            *reinterpret_cast<float4*>(m + (kL + L) * kT + 4 * q) = make_float4(hd.mT1[0], hd.mT1[1], hd.mT1[2], hd.mT1[3]);\n"
+     "          }\n"
+     "          asm volatile(\"s_waitcnt lgkmcnt(0)\" ::: \"memory\");\n"
+     "          if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n"
+     "        }\n"
+     "        __builtin_amdgcn_s_setprio(0);\n"
+     "      }\n"
+     "    }\n"
+     "  }\n"
+     "  for (int fb = 0; fb < c.nf; fb += lay.fc) {\n    const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;\n    if (fb > 0) {\n      scene_pos_dma<64 * (kRecW + NP)>"),
+    ("    for (int i = pw; i < nh; i += NP) {\n      const int fl = hb + hs * i;",
+     "    for (int i = pw + (fb == 0 ? peeled : 0); i < nh; i += NP) {\n      const int fl = hb + hs * i;"),
+]
 VARIANTS = {
     "base": {},
     "prev": {},   # prebuilt only: tools/ab/libg2k_prev.so (the last commit)
@@ -327,6 +368,8 @@ VARIANTS = {
     "nolsr": {"__flags__": ["-mllvm", "-disable-lsr"]},
     "no_recur": NO_RECUR_SCENE,
     "no_tiles": {SCENE: NO_TILES},
+    "peel": {SCENE: PEEL},
+    "tl_end_peel": {SCENE: lds_stamps(TL_END, head=False) + PEEL},
     "rec8": {SCENE: [("constexpr int kRecHeads = kRecW;", "constexpr int kRecHeads = 2 * kRecW;")]},
     "tl_end_rec8": {SCENE: lds_stamps(TL_END, head=False) + [("constexpr int kRecHeads = kRecW;", "constexpr int kRecHeads = 2 * kRecW;")]},
     "no_tile_mfma": {SCENE: [("      y0 = mfma4(a0[ks], w, y0);                           // Y[4q + v][n]\n      y1 = mfma4(L < kT ? a1[ks] : 0.f, w, y1);            // Y[16 + 4q + v][n] (0 for q >= 2)",
@@ -564,11 +607,11 @@ def main():
                 for _ in range(5):
                     plan.run()
             torch.cuda.synchronize()
-            W = 160 if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig", "tl_end_rec8") else 64
+            W = 160 if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig", "tl_end_rec8", "tl_end_peel") else 64
             buf = (ctypes.c_uint * (S * W))()
             assert lib.g2k_stamp_copy(buf, S * W) == 0
             st = np.frombuffer(buf, dtype=np.uint32).reshape(S, W).astype(np.int64)
-            {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print, "tl_end_orig": tl_end_print, "tl_end_rec8": tl_end_print}.get(name, tl_rec_print)(st, t)
+            {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print, "tl_end_orig": tl_end_print, "tl_end_rec8": tl_end_print, "tl_end_peel": tl_end_print}.get(name, tl_rec_print)(st, t)
             print(f"{name}: fwd {time_it(plan.run):7.2f} us (stamped build)")
             if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k"):
                 rel = (st - st[:, :1]) % (1 << 32)
