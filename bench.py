@@ -272,13 +272,16 @@ def timed_graph(step, n, warmup, dist, sync, stream):
 
 
 def graph_event_time(g, stream):
-    """Average seconds per step of a captured graph's replay (HIP events on its stream)."""
+    """Average seconds per step of a captured graph's replay, from HIP events
+    on the stream the replay is launched on (the current stream: the graph's
+    kernels run there, not on the capture stream)."""
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    cur = torch.cuda.current_stream()
     g.replay()
-    ev0.record(stream)
+    ev0.record(cur)
     g.replay()
-    ev1.record(stream)
+    ev1.record(cur)
     torch.cuda.synchronize()
     return ev0.elapsed_time(ev1) / 1e3 / g.n
 

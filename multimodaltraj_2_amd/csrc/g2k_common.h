@@ -45,13 +45,24 @@ constexpr int kBufOff = 0x7ffffff0;          // an offset no buffer here reaches
 __device__ __forceinline__ brsrc make_brsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
+// Cache policy of the kernels' output stores: sc1 (gfx950 CPol bits: sc0 1,
+// nt 2, sc1 16) — written through to the coherence point as they are made,
+// so the end-of-kernel release has no dirty L2 lines of ours to write back
+// (a whole launch's pred left in the XCDs' L2s cost ~1.3 us of write-back
+// per step at eth_hotel_synth: 16.75 -> 15.42 us with sc1).
+constexpr int kStoreAux = 16;
+// the same for a plain float store (a relaxed agent-scope atomic store is a
+// global_store ... sc1)
+__device__ __forceinline__ void store_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void bstore(brsrc r, int off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, kStoreAux);
 }
 __device__ __forceinline__ void bstore4(brsrc r, int off, float a, float b, float c, float d) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kStoreAux);
 }
 __device__ __forceinline__ float4 bload4(brsrc r, int off) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);

@@ -298,7 +298,7 @@ struct RecurH {
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) hs[(4 * q + i) * H + wv * kCols + 16 * t + L] = adj[i] * x[t][i];
+      for (int i = 0; i < 4; ++i) store_wt(hs + (4 * q + i) * H + wv * kCols + 16 * t + L, adj[i] * x[t][i]);
   }
 
   __device__ __forceinline__ void init_max(float* mred, int wv, int q, int L) const {

@@ -1304,7 +1304,7 @@ __device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCt
     }
     if (lane == 0) __hip_atomic_store(a.scene_ticket + c.s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (lane < 8) a.metrics[(size_t)c.s * 8 + lane] = v;
+  if (lane < 8) store_wt(a.metrics + (size_t)c.s * 8 + lane, v);
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
@@ -1499,7 +1499,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
         float x = acc4[v];
         if (nn < c.nact)
           x += fmaf(c.sVis[nn], ga[kGA_VE + L], c.sVis[Nmax + nn] * ga[kGA_VE + kD + L]);
-        row[nn * kD + L] = x;
+        store_wt(row + nn * kD + L, x);
       }
     }
   }
@@ -1541,7 +1541,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     } else {                                          // count of (frame, pedestrian) pairs
       for (int pr = 0; pr < NP + kRecW; ++pr) x += c.sMet[pr * 8 + 1];
     }
-    row[p] = x;
+    store_wt(row + p, x);
   }
 }
 

@@ -368,6 +368,10 @@ VARIANTS = {
     "nolsr": {"__flags__": ["-mllvm", "-disable-lsr"]},
     "no_recur": NO_RECUR_SCENE,
     "no_tiles": {SCENE: NO_TILES},
+    "st_nt": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 2;")]},
+    "st_sc1": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 16;")]},
+    "st_sys": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 17;")]},
+    "st_ntsc1": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 18;")]},
     "peel": {SCENE: PEEL},
     "tl_end_peel": {SCENE: lds_stamps(TL_END, head=False) + PEEL},
     "rec8": {SCENE: [("constexpr int kRecHeads = kRecW;", "constexpr int kRecHeads = 2 * kRecW;")]},
