@@ -582,10 +582,10 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   // (row max exchange: seq 1; e and its row partials into buffer 0: seq 2),
   // off the chain's critical path, which starts with the first heads after
   // the staging
+  if (live && c.nf > 0) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);   // (in the prologue's burst)
   if (c.nf > 0)
     scene_stage<NT, NP>(a, lay, c, 0, c.nf < lay.fc ? c.nf : lay.fc, [&] {
       if (!live) return;
-      rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);
       rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
       asm volatile("" ::: "memory");
       if (c.lane == 0) lds_store_flag(seq + c.wv, 1);
