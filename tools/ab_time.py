@@ -108,8 +108,8 @@ TL_FWD = [
     ("  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L,\n           c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);",
      "  rc.store(a.h_out + (size_t)c.s * kD * H, H, c.wv, c.q, c.L,\n           c.nf > 0 ? c.sRed + (c.nf & 1) * kRB : nullptr);\n  G2K_ST(26, " + R0 + ");\n"
      "  if (c.wv == 0 && c.lane == 0) g2k_stamp_buf[(size_t)c.s * 64 + 28] = (unsigned)__builtin_amdgcn_s_memrealtime();"),
-    ("      if (live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);\n    });",
-     "      if (live) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);\n    });\n  G2K_ST(52, " + R0 + ");"),
+    ("      if (c.lane == 0) lds_store_flag(seq + c.wv, 2);\n    });",
+     "      if (c.lane == 0) lds_store_flag(seq + c.wv, 2);\n    });\n  G2K_ST(52, " + R0 + ");"),
 ]
 
 
@@ -160,14 +160,26 @@ def lds_stamps(reps, head=True):
     return out
 
 
+# I-cache test: the recurrence waves' first head executed twice by the same
+# code (a loop, not unrolled), stamped before / between / after (R0)
+TL_ICACHE = [
+    ("    const int fl = c.wv;\n    const bool mine = c.X == 1 || fl % c.X == 0;\n    frame_head(",
+     "    const int fl = c.wv;\n    const bool mine = c.X == 1 || fl % c.X == 0;\n"
+     "    G2K_ST(76, " + R0 + ");\n"
+     "#pragma unroll 1\n    for (int rep = 0; rep < 2; ++rep) {\n    frame_head("),
+    ("               nullptr, c.L, c.q, /*want_m=*/false);\n    __builtin_amdgcn_s_setprio(0);\n  }\n",
+     "               nullptr, c.L, c.q, /*want_m=*/false);\n    G2K_ST(77 + rep, " + R0 + ");\n    }\n    __builtin_amdgcn_s_setprio(0);\n  }\n"),
+]
+
+
 # the producers' lead-in between the staging barrier and the first head
 TL_GAP = [
     ("    if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)",
      "    G2K_ST(70, " + P0 + " && fb == 0);\n    if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)\n    G2K_ST(71, " + P0 + " && fb == 0);"),
     ("    float rm[4];\n    scene_rm(lay, c, rm);\n    // phase 1",
      "    G2K_ST(72, " + P0 + " && fb == 0);\n    float rm[4];\n    scene_rm(lay, c, rm);\n    // phase 1"),
-    ("    if (fb == 0 && live) {\n      // softmax(h) numerators",
-     "    G2K_ST(74, " + R0 + " && fb == 0);\n    if (fb == 0 && live) {\n      // softmax(h) numerators"),
+    ("               nullptr, c.L, c.q, /*want_m=*/false);\n    __builtin_amdgcn_s_setprio(0);\n  }\n",
+     "               nullptr, c.L, c.q, /*want_m=*/false);\n    __builtin_amdgcn_s_setprio(0);\n  }\n  G2K_ST(74, " + R0 + ");\n"),
     ("    if (live) {\n      __builtin_amdgcn_s_setprio(2);",
      "    G2K_ST(75, " + R0 + " && fb == 0);\n    if (live) {\n      __builtin_amdgcn_s_setprio(2);"),
 ]
@@ -313,6 +325,38 @@ NO_RECUR = [("  const bool live = a.h_in != nullptr && c.x == 0;   // (the scene
 NO_TILES = [("    const int nitems = own.n * ntact > pw ? (own.n * ntact - pw + NP - 1) / NP : 0;   // forward",
              "    const int nitems = 0;")]
 NO_RECUR_SCENE = {SCENE: NO_RECUR}
+# the producers' heads before the tile set-up (mask bits, item counts, the
+# first targets' loads)
+_SETUP = """    if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
+    const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
+    ofo = own.fo;
+    const int nitems = own.n * ntact > pw ? (own.n * ntact - pw + NP - 1) / NP : 0;   // forward
+    // GRAD: this producer's own frames (ordinals) pw, pw + NP, ... < gend of
+    // the chunk (the last R own frames of the last chunk go to the
+    // recurrence waves)
+    const int R = GRAD && fb + lay.fc >= c.nf ? grad_rec_frames(own.n, NP) : 0;
+    const int gend = own.n - R;
+    // the first tiles' targets: in flight during the heads (GRAD: one buffer
+    // and the balancing stores, see grad_frames)
+    if (GRAD) {
+      load_targets(tgr, Nmax, c.nact, fb, own.fo + c.X * pw, 0, pw < gend, L, q, tgA, lay.tfb);
+      balance_stores<PM>(a);
+    } else {
+      load_item(fb, nitems, 0, tgA);
+      load_item(fb, nitems, 1, tgB);
+    }
+"""
+_SETUP_AFTER = _SETUP.replace("""    if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
+    const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
+    ofo = own.fo;
+""", """    if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
+    ofo = own.fo;
+""")
+HEADS_FIRST = [
+    (_SETUP, "    const OwnFrames own = own_frames(fb, cnt, c.X, c.x);\n"),
+    ("    // phase 2 — predictions and errors (GRAD: and the gradient)\n",
+     _SETUP_AFTER + "    // phase 2 — predictions and errors (GRAD: and the gradient)\n"),
+]
 # every producer's first head ahead of the chunk loop (and its set-up)
 PEEL = [
     ("  for (int fb = 0; fb < c.nf; fb += lay.fc) {\n    const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;\n    if (fb > 0) {\n      scene_pos_dma<64 * (kRecW + NP)>",
@@ -368,6 +412,8 @@ VARIANTS = {
     "nolsr": {"__flags__": ["-mllvm", "-disable-lsr"]},
     "no_recur": NO_RECUR_SCENE,
     "no_tiles": {SCENE: NO_TILES},
+    "heads_first": {SCENE: HEADS_FIRST},
+    "tl_end_hf": {SCENE: lds_stamps(TL_END, head=False) + HEADS_FIRST},
     "st_nt": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 2;")]},
     "st_sc1": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 16;")]},
     "st_sys": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 17;")]},
@@ -388,6 +434,7 @@ VARIANTS = {
     "tl_rec": {SCENE: TL_REC},
     "tl_lds": {SCENE: lds_stamps(TL_REC)},
     "tl_gap": {SCENE: lds_stamps(TL_REC + TL_GAP)},
+    "tl_icache": {SCENE: lds_stamps(TL_REC + TL_ICACHE)},
     "tl_tile": {SCENE: lds_stamps(TL_REC + TL_TILE)},
     "tl_b1": {SCENE: lds_stamps(TL_B1 + TL_REC)},
     "pos1k": {SCENE: POS1K},
@@ -611,13 +658,13 @@ def main():
                 for _ in range(5):
                     plan.run()
             torch.cuda.synchronize()
-            W = 160 if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig", "tl_end_rec8", "tl_end_peel") else 64
+            W = 160 if name in ("tl_lds", "tl_gap", "tl_icache", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k", "tl_end", "tl_end_orig", "tl_end_rec8", "tl_end_peel", "tl_end_hf") else 64
             buf = (ctypes.c_uint * (S * W))()
             assert lib.g2k_stamp_copy(buf, S * W) == 0
             st = np.frombuffer(buf, dtype=np.uint32).reshape(S, W).astype(np.int64)
-            {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print, "tl_end_orig": tl_end_print, "tl_end_rec8": tl_end_print, "tl_end_peel": tl_end_print}.get(name, tl_rec_print)(st, t)
+            {"tl_fwd": tl_fwd_print, "tl_end": tl_end_print, "tl_end_orig": tl_end_print, "tl_end_rec8": tl_end_print, "tl_end_peel": tl_end_print, "tl_end_hf": tl_end_print}.get(name, tl_rec_print)(st, t)
             print(f"{name}: fwd {time_it(plan.run):7.2f} us (stamped build)")
-            if name in ("tl_lds", "tl_gap", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k"):
+            if name in ("tl_lds", "tl_gap", "tl_icache", "tl_lds_warm", "tl_tile", "tl_b1", "tl_b1_pos1k"):
                 rel = (st - st[:, :1]) % (1 << 32)
                 med = np.median(rel, axis=0)
                 print("head 0 (median): operands", int(med[60]), "A done", int(med[61]), "attn done",
@@ -628,11 +675,14 @@ def main():
                     print("wave DMA issue start (median):", [int(med[96 + w]) for w in range(16)])
                     print("wave nact loaded (median):", [int(med[112 + w]) for w in range(16)])
                     print("wave at staging, before its DMA wait (median):", [int(med[128 + w]) for w in range(16)])
+                if name == "tl_icache":
+                    print("R0 head run twice (median): start", int(med[76]), "first done", int(med[77]),
+                          "second done", int(med[78]))
                 if name == "tl_gap":
                     print("P0 lead-in (median): B2", int(med[6]), "mask", int(med[70]), int(med[71]),
                           "targets issued", int(med[72]), "first head", int(med[7]), int(med[8]),
                           "second head", int(med[9]), int(med[10]),
-                          "| R0 at init", int(med[74]), "R0 init done", int(med[75]))
+                          "| R0 heads done", int(med[74]), "R0 chain start", int(med[75]))
                 if name == "tl_tile":
                     print("last tile (median): entry", int(med[40]), "Y", int(med[41]), "targets", int(med[42]),
                           "stores", int(med[43]), "errors", int(med[44]))
