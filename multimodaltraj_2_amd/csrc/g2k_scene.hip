@@ -1386,7 +1386,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       const int f = fb + fl;
       const bool mine = !all_heads || c.X == 1 || f % c.X == c.x;
       if (fl < nrh && !mine) continue;                   // (neither As nor M wanted here)
-      if (fl >= nrh && fl < kRecW + nrh) __builtin_amdgcn_s_setprio(1);
+      if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(1);   // the first round's heads
       const FrameHeadOut hd =
           frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                      c.sFlag + fl, f + 1,

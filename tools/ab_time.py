@@ -413,6 +413,12 @@ VARIANTS = {
     "no_recur": NO_RECUR_SCENE,
     "no_tiles": {SCENE: NO_TILES},
     "heads_first": {SCENE: HEADS_FIRST},
+    "prio12": {SCENE: [("      if (fl >= nrh && fl < kRecW + nrh) __builtin_amdgcn_s_setprio(1);",
+                        "      if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(1);")]},
+    "prio_all": {SCENE: [("      if (fl >= nrh && fl < kRecW + nrh) __builtin_amdgcn_s_setprio(1);",
+                          "      if (fl >= nrh) __builtin_amdgcn_s_setprio(1);")]},
+    "prio_split": {SCENE: [("      if (fl >= nrh && fl < kRecW + nrh) __builtin_amdgcn_s_setprio(1);",
+                            "      if (fl >= nrh) __builtin_amdgcn_s_setprio(fl < kRecW + nrh ? 2 : 1);")]},
     "tl_end_hf": {SCENE: lds_stamps(TL_END, head=False) + HEADS_FIRST},
     "st_nt": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 2;")]},
     "st_sc1": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 16;")]},
