@@ -21,23 +21,45 @@ __device__ __forceinline__ float grad_at(const float* g, int i) {
   return g[i];
 }
 
-template <bool COH>
+constexpr int kPre = 8;   // entries per thread held in registers (n <= 8192)
+
+// this thread's parameters and mean squares (entries tid + 1024 j), loaded
+// ahead of the gradient they are updated with
+__device__ __forceinline__ void load_update_state(const float* __restrict__ params,
+                                                  const float* __restrict__ ms, int n,
+                                                  float (&pp)[kPre], float (&pm)[kPre]) {
+#pragma unroll
+  for (int j = 0; j < kPre; ++j) {
+    const int i = threadIdx.x + j * 1024;
+    pp[j] = i < n ? params[i] : 0.f;
+    pm[j] = (ms && i < n) ? ms[i] : 0.f;
+  }
+}
+
+// PRE: pp / pm already hold this thread's parameters and mean squares
+// (load_update_state; n <= kPre * 1024)
+template <bool COH, bool PRE = false>
 __device__ __forceinline__ void update_body(float* __restrict__ params, float* __restrict__ ms,
                                             const float* __restrict__ grad, int n, float lr,
-                                            float decay, float clip, float* red) {
+                                            float decay, float clip, float* red,
+                                            float (*ppre)[kPre] = nullptr,
+                                            float (*pmre)[kPre] = nullptr) {
   const int tid = threadIdx.x;
   // up to kPre entries per thread: parameters and mean squares are loaded
   // together with the gradient, before the norm's reduction
-  constexpr int kPre = 8;
   const bool pre = n <= kPre * 1024;
   float pg[kPre], pp[kPre], pm[kPre];
   if (pre) {
+    if (PRE) {
+#pragma unroll
+      for (int j = 0; j < kPre; ++j) { pp[j] = (*ppre)[j]; pm[j] = (*pmre)[j]; }
+    } else {
+      load_update_state(params, ms, n, pp, pm);
+    }
 #pragma unroll
     for (int j = 0; j < kPre; ++j) {
       const int i = tid + j * 1024;
       pg[j] = i < n ? grad_at<COH>(grad, i) : 0.f;
-      pp[j] = i < n ? params[i] : 0.f;
-      pm[j] = (ms && i < n) ? ms[i] : 0.f;
     }
   }
   const float inv = 1.0f / fmaxf(grad_at<COH>(grad, n + 1), 1.0f);
@@ -111,6 +133,11 @@ __global__ void __launch_bounds__(kRowCols * kRowSlices) g2k_grad_rows_kernel(co
   __shared__ int last;
   const int c = threadIdx.x % kRowCols, sl = threadIdx.x / kRowCols;
   const int p = blockIdx.x * kRowCols + c;
+  // UPD: the update's parameters and mean squares in flight with the rows
+  // (only the last workgroup uses them: one memory round trip off its tail)
+  float pp[kPre], pm[kPre];
+  const bool pre = UPD && width - 2 <= kPre * 1024;
+  if (pre) load_update_state(up.params, up.ms, width - 2, pp, pm);
   float acc = 0.f;
   if (p < width) {
     for (int r0 = sl; r0 < S; r0 += 8 * kRowSlices) {
@@ -146,7 +173,11 @@ __global__ void __launch_bounds__(kRowCols * kRowSlices) g2k_grad_rows_kernel(co
   // under the HIP memory model, not just by gfx950's store ordering (their
   // write-through stores completed, vmcnt(0), before their ticket increments)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  update_body<true>(up.params, up.ms, grad, width - 2, up.lr, up.decay, up.clip, &red[0][0]);
+  if (pre)
+    update_body<true, true>(up.params, up.ms, grad, width - 2, up.lr, up.decay, up.clip, &red[0][0],
+                            &pp, &pm);
+  else
+    update_body<true>(up.params, up.ms, grad, width - 2, up.lr, up.decay, up.clip, &red[0][0]);
 }
 
 __global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ params,
