@@ -234,24 +234,28 @@ class GraphSteps:
     per-launch cost (Python, the C ABI's checks, hipLaunchKernel) no longer
     paces a ~20 us step.  ``run(i)`` with i a multiple of ``n`` replays it."""
 
-    def __init__(self, step, n, stream, i0=0):
+    def __init__(self, step, n, stream, i0=0, side=()):
         self.n = n
         self.g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
         with torch.cuda.graph(self.g, stream=stream):
+            for s in side:                     # forked from the capture stream ...
+                s.wait_stream(stream)
             for i in range(n):
                 step(i0 + i)
+            for s in side:                     # ... and joined back
+                stream.wait_stream(s)
         torch.cuda.synchronize()
 
     def replay(self):
         self.g.replay()
 
 
-def timed_graph(step, n, warmup, dist, sync, stream):
+def timed_graph(step, n, warmup, dist, sync, stream, side=()):
     """timed() with the warm-up and the timed steps each as one graph replay
     (exactly ``n`` steps between the barriers)."""
-    gw = GraphSteps(step, max(warmup, 1), stream)
-    gm = GraphSteps(step, n, stream, i0=max(warmup, 1))
+    gw = GraphSteps(step, max(warmup, 1), stream, side=side)
+    gm = GraphSteps(step, n, stream, i0=max(warmup, 1), side=side)
     gw.replay()
     sync()
     if dist is not None:
@@ -363,6 +367,10 @@ def main(argv=None):
     ap.add_argument("--split", type=int, default=0,
                     help="workgroups per scene (G2K_STEP_SPLIT; 0: automatic, enough to cover "
                          "the CUs when a rank has fewer scenes than CUs)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="reference mode: consecutive (independent) batches on this many "
+                         "streams in turn, so one launch's start overlaps the previous one's "
+                         "end (the roofline still divides by one launch's duration)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from the host instead of replaying the timed steps "
                          "from a HIP graph")
@@ -414,6 +422,8 @@ def main(argv=None):
                   split=args.split)
     abytes = algorithmic_bytes(b, H, pbytes, shared)
     K = args.rotate or max(1, -(-MALL_BYTES // abytes) + 1)
+    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(max(args.streams, 1) - 1)]
+    K = -(-K // len(streams)) * len(streams)     # batch k always on stream k % streams
 
     # K device-resident input batches (the base batch plus small per-batch
     # position offsets, so no two share a cache line) and their plans
@@ -434,8 +444,8 @@ def main(argv=None):
         batches.append(t)
         plans.append(fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"],
                                  t["n_active"], t["h0"], n_frames=t["n_frames"],
-                                 ped_mask=t["ped_mask"], stride=b.stride, out=out, stream=stream,
-                                 **layout))
+                                 ped_mask=t["ped_mask"], stride=b.stride, out=out,
+                                 stream=streams[k % len(streams)], **layout))
 
     def step(i):
         plans[i % K].run()
@@ -443,16 +453,22 @@ def main(argv=None):
     if args.no_graph:
         elapsed = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
     else:
-        elapsed, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream)
+        elapsed, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream,
+                                  side=streams[1:])
     # reference mode: replicas only; the ADE/FDE numerators of the last batch
     # are summed across ranks once at the end
     tot = plans[(args.steps - 1) % K].out.metrics.double().sum(dim=0)
     if dist is not None:
         dist.all_reduce(tot)
+    # the roofline's time: ONE launch's duration, launches back to back on
+    # one stream (no overlap; what rocprofv3 reports per dispatch), over the
+    # batches of stream 0
+    R = max(20, min(args.steps, 200))
+    one = [plans[k] for k in range(0, K, len(streams))]
     if args.no_graph:
-        kern_s = event_time(step, max(20, min(args.steps, 200)), stream)
+        kern_s = event_time(lambda i: one[i % len(one)].run(), R, stream)
     else:
-        kern_s = graph_event_time(gm, stream)
+        kern_s = graph_event_time(GraphSteps(lambda i: one[i % len(one)].run(), R, stream), stream)
     achieved = abytes / kern_s / 1e9
 
     train = None
@@ -486,6 +502,7 @@ def main(argv=None):
                        "hidden": H, "D": 16, "parallelism": f"dp{world}",
                        "input_batches_rotated": K, "pred_layout": args.pred_layout,
                        "targets_shared": shared, "workgroups_per_scene": split_of(S, F, args.split),
+                       "streams": len(streams),
                        "launch": "host launch per step" if args.no_graph else
                                  "HIP graph of the timed steps (one replay)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -413,6 +413,8 @@ VARIANTS = {
     "no_recur": NO_RECUR_SCENE,
     "no_tiles": {SCENE: NO_TILES},
     "heads_first": {SCENE: HEADS_FIRST},
+    "headprio2": {SCENE: [("      if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(1);   // the first round's heads",
+                           "      if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(2);")]},
     "prio12": {SCENE: [("      if (fl >= nrh && fl < kRecW + nrh) __builtin_amdgcn_s_setprio(1);",
                         "      if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(1);")]},
     "prio_all": {SCENE: [("      if (fl >= nrh && fl < kRecW + nrh) __builtin_amdgcn_s_setprio(1);",
