@@ -1,0 +1,10 @@
+# The round-end driver's sequence on one box: GPU tests, smoke, the default
+# bench line (CPU baseline included).   tools/gpu_final.sh TAG
+set -o pipefail
+O=gpurun_out/$1; mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -60 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; cat $O/smoke.log; exit 1; }
+tail -3 $O/smoke.log
+timeout -k 10 400 python bench.py > $O/bench.log 2>&1 || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }
+grep '^{' $O/bench.log | cut -c1-600
