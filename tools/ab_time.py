@@ -402,9 +402,9 @@ VARIANTS = {
     "base": {},
     "prev": {},   # prebuilt only: tools/ab/libg2k_prev.so (the last commit)
     "orig": {},
-    "no_finalize": {SCENE: [("  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);",
-                             "  return;\n  poll_word(c.sTicket, NP);\n  grad_priv_sum(c, NP);")]},
-    "no_frame_grad": {SCENE: [("        frame_grad(a, lay, c, pw + fi * NP, dm);", "")]},
+    "no_finalize": {SCENE: [("  poll_word(c.sTicket, NP + kRecW);\n  grad_priv_sum(c, NP);",
+                             "  return;\n  poll_word(c.sTicket, NP + kRecW);\n  grad_priv_sum(c, NP);")]},
+    "no_frame_grad": {SCENE: [("    frame_grad(a, lay, c, fl, dm, slot);", "")]},
     "no_tile_grad": {SCENE: [("  if (GRAD) {\n#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      d0[v] = has_t",
                               "  dWoT = f32x4{0.f, 0.f, 0.f, 0.f};\n  if (false) {\n#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      d0[v] = has_t")]},
     "stamps": {SCENE: STAMPS},
@@ -465,6 +465,10 @@ VARIANTS = {
     "recprio1": {SCENE: [("      __builtin_amdgcn_s_setprio(2);\n      const float* as_lane", "      __builtin_amdgcn_s_setprio(1);\n      const float* as_lane")]},
     "recprio3": {SCENE: [("      __builtin_amdgcn_s_setprio(2);\n      const float* as_lane", "      __builtin_amdgcn_s_setprio(3);\n      const float* as_lane")]},
     "headprio": {SCENE: [("      if (fl < kRecW) __builtin_amdgcn_s_setprio(1);", "      __builtin_amdgcn_s_setprio(1);")]},
+    # train mode at 16 waves (12 producers; the 128-VGPR cap spills)
+    "np12t": {SCENE: [("  return grad ? 8 : 12;", "  return grad && H > 128 ? 8 : 12;"),
+                      ("    if (NP == 8) {\n      switch (tpw) {\n        case 1: launch_k<1, 8, true>",
+                       "    if (NP == 12 && tpw == 2) { launch_k<2, 12, true>(a, l, st); return G2K_OK; }\n    if (NP == 8) {\n      switch (tpw) {\n        case 1: launch_k<1, 8, true>")]},
     "np12": {SCENE: [("  return (H >= 256 || Nmax >= 64) ? 12 : 8;", "  return 12;")]},
     "np12ts": {SCENE: [("  return (H >= 256 || Nmax >= 64) ? 12 : 8;", "  return 12;"),
                        ("pred_tile<false, NP == 8>", "pred_tile<false, true>"),
