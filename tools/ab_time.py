@@ -466,6 +466,10 @@ VARIANTS = {
     "recprio3": {SCENE: [("      __builtin_amdgcn_s_setprio(2);\n      const float* as_lane", "      __builtin_amdgcn_s_setprio(3);\n      const float* as_lane")]},
     "headprio": {SCENE: [("      if (fl < kRecW) __builtin_amdgcn_s_setprio(1);", "      __builtin_amdgcn_s_setprio(1);")]},
     # train mode at 16 waves (12 producers; the 128-VGPR cap spills)
+    # LLVM scheduling strategies for the whole library
+    "s_ilp": {"__flags__": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]},
+    "s_memclause": {"__flags__": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]},
+    "s_trackers": {"__flags__": ["-mllvm", "-amdgpu-use-amdgpu-trackers"]},
     "np12t": {SCENE: [("  return grad ? 8 : 12;", "  return grad && H > 128 ? 8 : 12;"),
                       ("    if (NP == 8) {\n      switch (tpw) {\n        case 1: launch_k<1, 8, true>",
                        "    if (NP == 12 && tpw == 2) { launch_k<2, 12, true>(a, l, st); return G2K_OK; }\n    if (NP == 8) {\n      switch (tpw) {\n        case 1: launch_k<1, 8, true>")]},

@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout
 tail -2 $O/pytest.log
 fi
 for c in "$@"; do
-  timeout -k 10 300 python tools/ab_time.py --rounds 5 $c ${AB_VARIANTS:-orig base} > $O/ab_$c.log 2>&1 || { echo "ab $c failed"; tail -20 $O/ab_$c.log; exit 1; }
+  timeout -k 10 300 python tools/ab_time.py --rounds ${AB_ROUNDS:-5} $c ${AB_VARIANTS:-orig base} > $O/ab_$c.log 2>&1 || { echo "ab $c failed"; tail -20 $O/ab_$c.log; exit 1; }
   grep median $O/ab_$c.log
 done
 for v in ${AB_TL:-tl_end_orig tl_end}; do
