@@ -422,10 +422,11 @@ VARIANTS = {
     "prio_split": {SCENE: [("      if (fl >= nrh && fl < kRecW + nrh) __builtin_amdgcn_s_setprio(1);",
                             "      if (fl >= nrh) __builtin_amdgcn_s_setprio(fl < kRecW + nrh ? 2 : 1);")]},
     "tl_end_hf": {SCENE: lds_stamps(TL_END, head=False) + HEADS_FIRST},
-    "st_nt": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 2;")]},
-    "st_sc1": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 16;")]},
-    "st_sys": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 17;")]},
-    "st_ntsc1": {"g2k_common.h": [("constexpr int kStoreAux = 0;", "constexpr int kStoreAux = 18;")]},
+    # output store cache policy (the product writes through: kStoreAux = 16, sc1)
+    "st_plain": {"g2k_common.h": [("constexpr int kStoreAux = 16;", "constexpr int kStoreAux = 0;")]},
+    "st_nt": {"g2k_common.h": [("constexpr int kStoreAux = 16;", "constexpr int kStoreAux = 2;")]},
+    "st_sys": {"g2k_common.h": [("constexpr int kStoreAux = 16;", "constexpr int kStoreAux = 17;")]},
+    "st_ntsc1": {"g2k_common.h": [("constexpr int kStoreAux = 16;", "constexpr int kStoreAux = 18;")]},
     "peel": {SCENE: PEEL},
     "tl_end_peel": {SCENE: lds_stamps(TL_END, head=False) + PEEL},
     "rec8": {SCENE: [("constexpr int kRecHeads = kRecW;", "constexpr int kRecHeads = 2 * kRecW;")]},
