@@ -487,6 +487,14 @@ VARIANTS = {
     "warm": {SCENE: WARM},
     "tl_lds_warm": {SCENE: lds_stamps(TL_REC) + WARM},
 }
+# variants of earlier experiments whose anchors no longer match the sources
+# (their measurements are recorded in DESIGN.md §9 and profiles/): out of
+# the runnable set until re-anchored
+STALE = ('no_tile_grad', 'stamps', 'stamps_norecur', 'prio12', 'prio_all', 'prio_split',
+         'rec8', 'tl_end_rec8', 'no_pred_store', 'stamps_nolsr', 'stamps_tile', 'stamps_fwd',
+         'tl_tile', 'pos1k', 'fullseg', 'headprio', 'np12', 'np12ts', 'tl_b1_pos1k', 'warm', 'tl_lds_warm')
+for _k in STALE:
+    VARIANTS.pop(_k)
 
 
 AB_DIR = os.path.join(ROOT, "tools", "ab")   # prebuilt variant libraries (git-ignored; travel to the box)
