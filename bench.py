@@ -291,14 +291,26 @@ def graph_event_time(g, stream):
 
 
 def load_pmc(name):
-    p = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
+    """(HBM bytes per launch, provenance) from the committed PMC profile
+    profiles/pmc_<name>.json — a STATIC value, collected by tools/gpu_round.sh
+    in separate rocprofv3 --pmc passes (FETCH_SIZE x2 + WRITE_SIZE), not in this
+    run; ``matches_current_tree`` says whether it was taken on the kernel
+    sources this run built from (build.kernel_tree_sha)."""
+    from multimodaltraj_2_amd.build import kernel_tree_sha
+    rel = os.path.join("profiles", f"pmc_{name}.json")
+    p = os.path.join(ROOT, rel)
     if not os.path.exists(p):
-        return None
+        return None, None
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
+    sha = d.get("kernel_tree_sha")
+    return d.get("hbm_bytes_per_launch"), {
+        "file": rel, "kind": "static profile (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                            "of bench.py, tools/gpu_round.sh), not measured in this run",
+        "kernel_tree_sha": sha, "matches_current_tree": sha == kernel_tree_sha()}
 
 
 def real_scene_batch(S, H, rank, world):
@@ -477,6 +489,7 @@ def main(argv=None):
                            stream)
 
     if rank == 0:
+        pmc = load_pmc(args.config)
         m = tot.cpu().numpy()
         line = {
             "metric": METRIC,
@@ -501,13 +514,13 @@ def main(argv=None):
                        "frames_per_step": b.frames, "obs_len": 8, "pred_len": 12, "Nmax": Nmax,
                        "hidden": H, "D": 16, "parallelism": f"dp{world}",
                        "input_batches_rotated": K, "pred_layout": args.pred_layout,
-                       "targets_shared": shared, "workgroups_per_scene": split_of(S, F, args.split),
+                       "targets_shared": shared, "workgroups_per_scene": fs.step_split(S, F, H, Nmax, b.pos.shape[1], b.stride, args.split),
                        "streams": len(streams),
                        "launch": "host launch per step" if args.no_graph else
                                  "HIP graph of the timed steps (one replay)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_pmc(args.config),
+                         "traffic": pmc[0], "traffic_source": pmc[1],
                          "kernel": "g2k_step_fused_f32 (g2k_scene_kernel)",
                          "kernel_us": kern_s * 1e6, "algorithmic_bytes": abytes},
             "cpu_baseline": cpu,
@@ -524,12 +537,6 @@ def main(argv=None):
     if dist is not None:
         dist.destroy_process_group()
     return 0
-
-
-def split_of(S, F, requested):
-    """Workgroups per scene the launch uses (scene_split, csrc/g2k_common.h)."""
-    x = requested or (1 if S >= 256 else 256 // max(S, 1))
-    return max(1, min(x, 4, max(F, 1)))
 
 
 def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, layout, stream):
@@ -565,6 +572,7 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
     gl = last["g"].double().cpu().numpy()
     abytes = train_algorithmic_bytes(b, H, pbytes, ts.P, layout["targets_shared"])
     achieved = abytes / kern_s / 1e9
+    pmc = load_pmc(args.config + "_train")
     return {"metric": f"frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + "
                       f"{'L2' if args.loss == 'l2' else 'bivariate-Gaussian NLL'} loss gradient + "
                       "gradient all-reduce + RMSProp update", "loss": args.loss,
@@ -574,7 +582,7 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
             "optimizer": "RMSProp lr 0.005 decay 0.95, global-norm clip 10 (argParser.py:38-47)",
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_pmc(args.config + "_train"),
+                         "traffic": pmc[0], "traffic_source": pmc[1],
                          "kernel": ts.kernel_names, "step_us": kern_s * 1e6,
                          "algorithmic_bytes": abytes}}
 

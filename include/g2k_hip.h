@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define G2K_ABI_VERSION 4
+#define G2K_ABI_VERSION 5
 
 enum {
   G2K_OK = 0,
@@ -75,12 +75,15 @@ typedef struct g2k_dims {
  * (P = 24 Nmax + 496 + 36, the head's 36 after Wo). */
 #define G2K_STEP_LOSS_NLL 4
 /* Workgroups per scene (bits 8..10): G2K_STEP_SPLIT(x), x in 1..4, or 0 =
- * automatic (x = min(4, 256 / S), at most F: a launch of fewer scenes than
- * the device has CUs spreads each scene's frames over x workgroups, the
- * first of which also runs the recurrence).  x > 1 needs the workspace
- * (g2k_step_workspace_bytes / g2k_train_workspace_bytes /
- * g2k_grad_workspace_bytes) zero-filled before its first use; every call
- * leaves it zero-filled again. */
+ * automatic (x = min(4, CUs / S) for the current device's CU count — 256 on
+ * MI355X, 256 assumed without a device — at most F: a launch of fewer scenes
+ * than the device has CUs spreads each scene's frames over x workgroups, the
+ * first of which also runs the recurrence; g2k_step_split reports x).  x > 1
+ * needs the workspace (g2k_step_workspace_bytes / g2k_train_workspace_bytes /
+ * g2k_grad_workspace_bytes) zero-filled before its first use, in stream order
+ * with the first launch (g2k_workspace_init: a memset on the launch stream);
+ * every call leaves it zero-filled again.  One workspace per stream: two
+ * launches in flight must not share one. */
 #define G2K_STEP_SPLIT_SHIFT 8
 #define G2K_STEP_SPLIT_MASK (7 << G2K_STEP_SPLIT_SHIFT)
 #define G2K_STEP_SPLIT(x) ((x) << G2K_STEP_SPLIT_SHIFT)
@@ -107,6 +110,12 @@ int64_t g2k_step_lds_bytes(const g2k_dims* d);
 /* Bytes of caller-provided device workspace g2k_step_fused_f32 needs for `d`
  * (0: every intermediate stays on chip); -1 on invalid dims. */
 int64_t g2k_step_workspace_bytes(const g2k_dims* d);
+/* Workgroups per scene the step / train entry points use for `d` (the
+ * G2K_STEP_SPLIT request, or the automatic choice); -1 on invalid dims. */
+int32_t g2k_step_split(const g2k_dims* d);
+/* Zero-fill `workspace_bytes` bytes of a workspace on `stream` (hipMemsetAsync):
+ * the stream-ordered first fill the split tickets need. */
+int g2k_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
  * g2k_step_fused_f32 — the whole per-frame body of train.py:197-276 for S
@@ -334,12 +343,17 @@ int g2k_context_conv_f32(const float* img, int32_t Hh, int32_t Ww, int32_t C, co
  * Tensorized data path (a1/a2 of §8(a)).  Host-side
  * planning (no device memory, callable without a GPU) plus one device gather.
  *
- * g2k_traj_create: index over one CSV split — `frame` / `ped` are rows 0 / 1 of
- *   the split's columns (load_traj.py:133-139: tr_data or val_data), `diff` =
- *   obs_len.  Keys are every frame value plus the grid seed + k*diff <= max;
- *   grid keys hold their columns in file order, the others are empty
- *   (load_traj.py:234-256 frame_preprocess).  Returns an opaque handle, NULL on
- *   failure.  g2k_traj_destroy frees it.
+ * g2k_traj_create: index over the columns the frame dict is built from —
+ *   `frame` / `ped` are rows 0 / 1 of those columns, `diff` = obs_len.  Keys are
+ *   every frame value plus the grid seed + k*diff <= max; grid keys hold their
+ *   columns in file order, the others are empty (load_traj.py:234-256
+ *   frame_preprocess).  The reference reads the dict from trajectories_0.cpkl
+ *   (load_traj.py:95-112), which for every shipped dataset is frame_preprocess
+ *   over the WHOLE CSV (the pickles' bytes equal that dict's); eth/univ
+ *   has no pickle and is built over the split.  `walk_max` = next_step's bound
+ *   max(self.frameList) (load_traj.py:163, 104: the split's, tr_data or
+ *   val_data, >= 1).  Returns an opaque handle, NULL on failure.
+ *   g2k_traj_destroy frees it.  (ABI 5: `walk_max` added.)
  * g2k_traj_next_step: DataLoader.next_step (load_traj.py:153-224) from
  *   `frame_pointer`: keys[n_keys] = the batch's (non-empty) frame keys in
  *   x_batch order; the target draws as the drawn frames' columns one frame after
@@ -356,7 +370,8 @@ int g2k_context_conv_f32(const float* img, int32_t Hh, int32_t Ww, int32_t C, co
  *   extra nodes are dropped), n_keys [n] = len(batch), next_pointer [n] or NULL.
  *   Node order is the graph's insertion order.
  * g2k_scene_gather_f32: expands those plans on the device: xy [cols, 2] (rows
- *   2:4 of the split, fp32), vis [2, cols] or NULL (rows 4:6; ETH: none, Q14)
+ *   2:4 of the index's columns, fp32), vis [2, cols] or NULL (rows 4:6; ETH:
+ *   none, Q14)
  *   -> pos [S, 8, Nmax, 2] (slot -1: 0), vislet [S, 2, Nmax] = vis[:, vis_off[s]
  *   + n] (train.py:182 / sample.py:184; vis_off NULL = 0), targets
  *   [S, F, Nmax, 12, 2] (the same 12 points for every frame: the reference
@@ -364,7 +379,8 @@ int g2k_context_conv_f32(const float* img, int32_t Hh, int32_t Ww, int32_t C, co
  *   (1: n < n_active and all 12 target columns present).  Columns >= n_active
  *   are zero.
  */
-void* g2k_traj_create(const double* frame, const double* ped, int64_t cols, int32_t diff);
+void* g2k_traj_create(const double* frame, const double* ped, int64_t cols, int32_t diff,
+                      double walk_max);
 void g2k_traj_destroy(void* traj);
 int g2k_traj_next_step(const void* traj, double frame_pointer, int32_t batch_size, int32_t obs_len,
                        double* keys, int32_t max_keys, int32_t* n_keys, int64_t* draw_cols,

@@ -43,6 +43,8 @@ SYMBOLS = {
     "g2k_last_error": (ctypes.c_char_p, []),
     "g2k_step_lds_bytes": (c_i64, [ctypes.POINTER(G2KDims)]),
     "g2k_step_workspace_bytes": (c_i64, [ctypes.POINTER(G2KDims)]),
+    "g2k_step_split": (ctypes.c_int32, [ctypes.POINTER(G2KDims)]),
+    "g2k_workspace_init": (c_int, [c_vp, c_i64, c_vp]),
     "g2k_step_fused_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_vp]),
@@ -77,7 +79,7 @@ SYMBOLS = {
     "g2k_context_conv_workspace_bytes": (c_i64, [c_i32, c_i32, c_i32]),
     "g2k_context_conv_f32": (c_int, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp,
                                      c_vp, c_i64, c_vp]),
-    "g2k_traj_create": (c_vp, [c_vp, c_vp, c_i64, c_i32]),
+    "g2k_traj_create": (c_vp, [c_vp, c_vp, c_i64, c_i32, ctypes.c_double]),
     "g2k_traj_destroy": (None, [c_vp]),
     "g2k_traj_next_step": (c_int, [c_vp, ctypes.c_double, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp,
                                    c_i64, c_vp, c_vp, c_vp]),
@@ -87,7 +89,7 @@ SYMBOLS = {
                                      c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class G2KLibraryError(RuntimeError):

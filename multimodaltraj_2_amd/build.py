@@ -31,6 +31,19 @@ def flags_for(src):
     return FLAGS + FILE_FLAGS.get(os.path.basename(src), [])
 
 
+def kernel_tree_sha() -> str:
+    """sha256 over the library's sources (csrc/*.hip, *.cpp, *.h and the ABI
+    header), names and bytes: identifies the kernel tree a profile was taken
+    on (tools/collect_pmc.py records it, bench.py compares)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(SRC + CXX_SRC + HDR):
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True

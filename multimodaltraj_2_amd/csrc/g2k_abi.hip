@@ -21,6 +21,25 @@ int set_err(int code, const char* fmt, ...) {
   return code;
 }
 
+int device_cus() {
+  // hipDeviceAttributeMultiprocessorCount of the current device, cached per
+  // device (256, MI355X's count, when no device is visible: host-only planning)
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  int n = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) {
+    (void)hipGetLastError();
+    n = 256;
+  }
+  __atomic_store_n(&cache[dev], n, __ATOMIC_RELAXED);
+  return n;
+}
+
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess)
@@ -156,9 +175,23 @@ int64_t g2k_step_lds_bytes(const g2k_dims* d) {
   return scene_lds_bytes(d, false);
 }
 
+int32_t g2k_step_split(const g2k_dims* d) {
+  if (validate_common(d, true, false, kTrainFlags) != G2K_OK) return -1;
+  return scene_split(*d);
+}
+
 int64_t g2k_step_workspace_bytes(const g2k_dims* d) {
   if (validate_common(d, true, false, kStepFlags) != G2K_OK) return -1;
   return split_ws_bytes(*d);   // one workgroup per scene: every intermediate stays on chip
+}
+
+int g2k_workspace_init(void* workspace, int64_t workspace_bytes, void* stream) {
+  if (workspace_bytes < 0 || (workspace_bytes > 0 && !workspace))
+    return set_err(G2K_EINVAL, "workspace_init: bad arguments");
+  if (workspace_bytes == 0) return G2K_OK;
+  if (hipMemsetAsync(workspace, 0, (size_t)workspace_bytes, (hipStream_t)stream) != hipSuccess)
+    return set_err(G2K_ELAUNCH, "workspace_init: memset failed");
+  return G2K_OK;
 }
 
 int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,

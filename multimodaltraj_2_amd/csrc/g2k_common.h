@@ -412,13 +412,16 @@ struct StepArgs {
 };
 
 // Workgroups per scene of the fused step (G2K_STEP_SPLIT, include/g2k_hip.h):
-// the requested count, else enough to cover the device's 256 CUs (4 at most),
-// never more than the frames to share.
-constexpr int kSceneCUs = 256;
+// the requested count, else enough to cover the current device's CUs (4 at
+// most), never more than the frames to share.
 constexpr int kMaxSplit = 4;
+int device_cus();   // CUs of the current device (g2k_abi.hip; 256 without a device)
 inline int scene_split(const g2k_dims& d) {
   int x = (d.flags & G2K_STEP_SPLIT_MASK) >> G2K_STEP_SPLIT_SHIFT;
-  if (x == 0) x = d.S >= kSceneCUs ? 1 : (d.S > 0 ? kSceneCUs / d.S : 1);
+  if (x == 0) {
+    const int cus = device_cus();
+    x = d.S >= cus ? 1 : (d.S > 0 ? cus / d.S : 1);
+  }
   if (x > kMaxSplit) x = kMaxSplit;
   if (x > d.F) x = d.F;
   return x < 1 ? 1 : x;

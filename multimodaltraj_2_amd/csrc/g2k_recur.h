@@ -227,16 +227,23 @@ struct Recur {
 //   A.B + A'.B = sum_rows (a_hi + a_lo)(b_hi + b_lo)
 // (A and B index K by the same (lane group, slot), so the slot -> row map is
 // free; A' is two 64-bit moves).  Products are exact in the f32
-// accumulator; the split loses < 2^-21 relative per operand, and every term
-// is positive (As >= 0, e > 0), so a sum's relative error is at most its
-// terms' (DESIGN.md "recurrence numerics"; the parity tests keep the 1e-5 h
-// tolerance).
+// accumulator; what the split loses is the rounding of each lo part, and
+// every term is positive (As >= 0, e > 0).
 //
 // Range: the accumulator starts at -kOff (kOff = 7), so the exp2 of the
 // result is e_s = 2^-7 e, its row sums Z_s = 2^-7 Z and the A operand
-// b / Z_s = 128 As log2(e) / Z: both operands and their lo parts stay in the
-// f16 normal range for H = 64 .. 512 (Z ~ H + 1), with no scaling
-// instruction anywhere.  The last frame starts its accumulator at 0 instead:
+// b / Z_s = 128 As log2(e) / Z, with no scaling instruction anywhere.  The hi
+// parts are f16 normals, but the lo parts mostly are NOT: e_s lies in
+// [2^-7, 2^-5.6], so its lo part is below 2^-17 — an f16 subnormal, rounded
+// to 2^-24 spacing, i.e. <= 2^-25 absolute (~2^-18 relative to e_s), and the
+// same for the A operand's lo part.  The product's absolute error is then
+// <= 2^-25 (sum_k A_k + 16 max e_s): ~3e-6 of h' at H = 128 and ~6e-6 at
+// H = 512 in the worst case (all roundings aligned; DESIGN.md §6
+// "recurrence numerics").  kOff = 7 balances the two terms for H = 128 .. 512
+// (the optimum is 2^(2 kOff) ~ 30 Z): a smaller kOff shrinks the e term but
+// grows the A term by the same factor.  close_h's 1e-5 bound is checked at
+// H = 512 over 100 frames (tests/test_step_gpu.py); errors do not compound
+// across frames (every frame renormalises).  The last frame starts its accumulator at 0 instead:
 // its result is the output h' (an accumulator near -7 would hold h' log2(e)
 // ~ 0.01 with 2^-22 absolute resolution only), and the adj ratio it feeds is
 // scale-free.

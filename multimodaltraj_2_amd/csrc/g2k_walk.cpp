@@ -6,9 +6,13 @@
 // expands on the device into the step's [S, ...] tensors.
 //
 // Semantics are the reference's, including its quirks:
-//  * trajectories (load_traj.py:234-256): every frame value of the split is a
-//    key; keys seed + k*diff <= max(frame) hold that frame's rows in file order,
-//    the other keys are empty;
+//  * trajectories (load_traj.py:234-256): every frame value of the columns the
+//    dict was built over is a key; keys seed + k*diff <= max(frame) hold that
+//    frame's rows in file order, the other keys are empty.  The reference READS
+//    the dict from trajectories_0.cpkl (load_traj.py:95-112), which for the
+//    shipped datasets is frame_preprocess over the WHOLE CSV, while the walk's
+//    bound max(self.frameList) (load_traj.py:163) is the split's: the two
+//    ranges are separate arguments (`cols` columns, `walk_max`);
 //  * next_step: up to batch_size + 1 passes; pass p appends the keys fp, fp +
 //    diff, ... (batch_size keys, stopping at the first missing key) to a growing
 //    window, then walks the window with one cursor that advances once per
@@ -44,7 +48,8 @@ namespace {
 struct Traj {
   int64_t cols = 0;
   int32_t diff = 8;
-  double seed = 0, fmax = 0;
+  double seed = 0, fmax = 0;                 // the dict's grid: seed .. max over all columns
+  double walk_max = 0;                       // next_step's max(self.frameList), :163
   std::vector<int64_t> ped;                  // int(ped id) per column
   std::vector<int32_t> pid;                  // dense pedestrian index per column
   int32_t n_peds = 0;
@@ -84,7 +89,7 @@ void next_step(const Traj& T, double fp, int bs, int obs, Plan& P) {
     return had;
   };
   const double lg = log((double)T.diff);
-  const double max_idx = T.fmax;
+  const double max_idx = T.walk_max;
   const double max_log = log(max_idx) / lg;                     // :166
   double idx = fp;                                              // :167
   int64_t pc = 1;                                               // :162
@@ -190,8 +195,9 @@ using g2k::set_err;
 
 extern "C" {
 
-void* g2k_traj_create(const double* frame, const double* ped, int64_t cols, int32_t diff) {
-  if (!frame || !ped || cols < 1 || diff < 1) {
+void* g2k_traj_create(const double* frame, const double* ped, int64_t cols, int32_t diff,
+                      double walk_max) {
+  if (!frame || !ped || cols < 1 || diff < 1 || !(walk_max >= 1.0)) {
     set_err(G2K_EINVAL, "g2k_traj_create: bad arguments");
     return nullptr;
   }
@@ -204,6 +210,7 @@ void* g2k_traj_create(const double* frame, const double* ped, int64_t cols, int3
   T->diff = diff;
   T->seed = frame[0];                                   // load_traj.py:141
   T->fmax = frame[0];
+  T->walk_max = walk_max;
   T->ped.resize(cols);
   T->pid.resize(cols);
   std::unordered_map<int64_t, int32_t> dense;

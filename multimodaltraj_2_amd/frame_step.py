@@ -143,16 +143,32 @@ def step_lds_bytes(S, F, H, Nmax, W, stride) -> int:
     return int(lib.g2k_step_lds_bytes(ctypes.byref(d)))
 
 
+def step_split(S, F, H, Nmax, W, stride, split=0) -> int:
+    """Workgroups per scene the library uses (g2k_step_split: the request, or
+    the automatic choice from the current device's CU count)."""
+    lib = _lib.load()
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride,
+                     step_flags(split=split))
+    x = int(lib.g2k_step_split(ctypes.byref(d)))
+    if x < 1:
+        _lib.check("g2k_step_split", -1)
+    return x
+
+
 def step_workspace_bytes(S, F, H, Nmax, W, stride) -> int:
     lib = _lib.load()
     d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride)
     return int(lib.g2k_step_workspace_bytes(ctypes.byref(d)))
 
 
-def workspace(nbytes, device):
-    """A launch plan's own workspace, zero-filled (split scenes keep per-scene
-    tickets in it that every call leaves at zero; include/g2k_hip.h)."""
-    return torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+def workspace(nbytes, device, stream=None):
+    """A launch plan's own workspace, zero-filled ON THE PLAN'S STREAM (split
+    scenes keep per-scene tickets in it that every call leaves at zero, so the
+    first fill must be stream-ordered before the first launch, which may run
+    on a stream other than the current one; include/g2k_hip.h)."""
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    with torch.cuda.stream(s):
+        return torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
 def step_fused(params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
@@ -255,7 +271,7 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
     nws = int(lib.g2k_step_workspace_bytes(ctypes.byref(d)))
     if nws < 0:
         _lib.check("g2k_step_workspace_bytes", -1)
-    ws = workspace(nws, dev)
+    ws = workspace(nws, dev, stream)
     args = (ctypes.byref(d), ctypes.byref(w), _ptr(pos), _ptr(vislet), _ptr(G), _ptr(targets),
             _ptr(n_active), _ptr(n_frames), _ptr(ped_mask), _ptr(h), _ptr(out.h), _ptr(out.pred),
             _ptr(out.metrics), _ptr(out.attn), _ptr(out.cost), ctypes.c_float(lam),

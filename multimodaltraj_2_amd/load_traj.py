@@ -6,9 +6,17 @@ same batches, with the build decisions of SURVEY.md Appendix B:
 
 * Q8  — the data root is a parameter (``data_root``), not a hard-coded path;
 * Q18 — ``sel=None`` selects file 0 instead of prompting with ``input()``;
-* the frame dict (``trajectories``) is always rebuilt from the CSV with the
-  reference's own frame_preprocess arithmetic (load_traj.py:234-256); the
-  pickled ``trajectories_0.cpkl`` files are never loaded;
+* the frame dict (``trajectories``) is the one the reference READS: with
+  ``infer=False`` it loads ``trajectories_0.cpkl`` whenever that file exists
+  (load_traj.py:95-112), and each shipped pickle is frame_preprocess
+  (load_traj.py:234-256) over the WHOLE CSV — its bytes equal
+  ``pickle.dumps`` of that dict (tests/test_frame_dict.py, the file's sha256 in
+  tests/golden/data_*.npz), while the walk's bound ``max(self.frameList)``
+  (:163) and ``num_batches`` (:104) stay the 70 % split's.  Without a pickle
+  (eth/univ; every ``infer=True`` loader) the reference builds the dict over
+  the split it loaded.  The dict is rebuilt from the CSV here; the pickles are
+  never unpickled (``frame_dict="whole" | "split"``, default: as the
+  reference would find it);
 * ``next_step``'s mutable default ``targets={}`` (load_traj.py:153) is
   never mutated by the reference (its first insertion rebinds ``targets`` to
   a new dict, :216-217), so every call starts from an empty dict: ``None``
@@ -26,18 +34,23 @@ import os
 import numpy as np
 
 class TrajIndex:
-    """Native index over one CSV split (g2k_traj_create; csrc/g2k_walk.cpp):
-    the frame dict's keys and rows, and the reference's batch walk over them.
+    """Native index over the frame dict's columns (g2k_traj_create;
+    csrc/g2k_walk.cpp): the dict's keys and rows, and the reference's batch
+    walk over them.
     Host code only: usable without a GPU."""
 
-    def __init__(self, frames, peds, diff):
+    def __init__(self, frames, peds, diff, walk_max=None):
+        """``frames`` / ``peds``: rows 0 / 1 of the columns the frame dict
+        spans; ``walk_max``: next_step's max(self.frameList) (default: the
+        largest of ``frames``)."""
         from . import _lib
         self._lib = _lib.load()
         self.frames = np.ascontiguousarray(frames, dtype=np.float64)
         peds = np.ascontiguousarray(peds, dtype=np.float64)
         self.cols = int(self.frames.shape[0])
+        self.walk_max = float(self.frames.max() if walk_max is None else walk_max)
         self._h = self._lib.g2k_traj_create(self.frames.ctypes.data, peds.ctypes.data, self.cols,
-                                            int(diff))
+                                            int(diff), self.walk_max)
         if not self._h:
             _lib.check("g2k_traj_create", -1)
 
@@ -92,9 +105,16 @@ DATA_DIRS = ["eth/hotel/", "eth/univ/", "ucy/zara/zara01/", "ucy/zara/zara02/", 
 
 class DataLoader:
     def __init__(self, args, datasets=(0, 1, 2, 3, 4, 5, 6), sel=None, start=0,
-                 processFrame=False, infer=False, data_root=None, raw_data=None):
+                 processFrame=False, infer=False, data_root=None, raw_data=None,
+                 frame_dict=None):
         """load_traj.py:11-104.  ``raw_data`` (the CSV array) may be passed
-        directly (tests, fixtures) instead of reading ``data_root``."""
+        directly (tests, fixtures) instead of reading ``data_root``.
+        ``frame_dict``: "whole" (the dict over the whole CSV: what the shipped
+        trajectories_0.cpkl holds) or "split" (frame_preprocess over the loaded
+        split: what the reference builds when no pickle exists); default: "whole"
+        when the reference would load a pickle — from ``data_root``, when
+        ``<dir>/trajectories_<sel>.cpkl`` exists (``val_...`` with infer,
+        load_traj.py:72-95); with ``raw_data``, unless ``infer``."""
         self.data_dirs = [os.path.join(data_root or "", d) for d in DATA_DIRS]
         self.used_data_dirs = [self.data_dirs[x] for x in datasets]
         self.infer = infer
@@ -107,6 +127,16 @@ class DataLoader:
         self.diff = self.obs_len
         self.current_dir = self.used_data_dirs[start]
         self.dataset_pointer = 0 if sel is None else sel
+        if frame_dict is None:
+            if raw_data is not None:
+                frame_dict = "split" if infer else "whole"
+            else:
+                name = ("val_trajectories_{0}.cpkl" if infer else "trajectories_{0}.cpkl")
+                pk = os.path.join(self.current_dir, name.format(int(self.dataset_pointer)))
+                frame_dict = "whole" if os.path.exists(pk) else "split"   # :95-103
+        if frame_dict not in ("whole", "split"):
+            raise ValueError(f"frame_dict must be 'whole' or 'split', not {frame_dict!r}")
+        self.frame_dict = frame_dict
         if raw_data is not None:
             self._set_raw(np.asarray(raw_data, dtype=np.float64), val=infer)
         else:
@@ -136,7 +166,9 @@ class DataLoader:
         self.seed = self.frameList[0]
         self.frame_pointer = self.seed
         self._fmax = self.frameList.max()          # max(self.frameList), load_traj.py:163
-        self.index = TrajIndex(self.frameList, src[1, :], self.diff)
+        # the columns the frame dict spans (see the module docstring)
+        self.dict_data = raw if self.frame_dict == "whole" else src
+        self.index = TrajIndex(self.dict_data[0], self.dict_data[1], self.diff, walk_max=self._fmax)
 
     @property
     def trajectories(self):
@@ -147,20 +179,35 @@ class DataLoader:
         return self._traj
 
     def frame_preprocess(self, data_file=None, seed=0):
-        """load_traj.py:234-256: {frame: [{ped: [x, y]}, ...]}; every frame of
-        frameList is a key (empty dict), frames seed + k*diff get their peds."""
-        frame_data = {i: {} for i in self.frameList}
+        """load_traj.py:234-256 over the dict's columns (``dict_data``):
+        {frame: [{ped: [x, y]}, ...]}; every frame value is a key (empty dict),
+        frames seed + k*diff <= max get their peds."""
+        d = self.dict_data
+        frame_data = {i: {} for i in d[0]}
         # the rows of each frame index in file order, grouped in one pass (the
         # reference rescans every row per frame: same lists, O(rows) here)
         rows = {}
-        for (ind, ped, px, py) in np.transpose(self.pedsPerFrameList):
+        for (ind, ped, px, py) in np.transpose(d[0:4]):
             rows.setdefault(ind, []).append({ped: [px, py]})
         fp = self.seed
-        fmax = self._fmax
+        fmax = d[0].max()
         while fp <= fmax:
             frame_data[fp] = rows.get(fp, [])
             fp += self.diff
         return frame_data
+
+    def frame_dict_pickle(self):
+        """The bytes frame_preprocess writes for this dict (load_traj.py:254-256:
+        ``pickle.dump(frame_data, f, protocol=2)``) as the numpy 1.x the
+        reference ran under writes them: a scalar's reduce names
+        ``numpy.core.multiarray`` and the float64 dtype's constructor arguments
+        are the ints 0 / 1 (numpy >= 2 writes ``numpy._core`` and bools).  For
+        the shipped datasets these are the bytes of ``trajectories_0.cpkl``."""
+        import pickle
+        b = pickle.dumps(self.trajectories, protocol=2)
+        b = b.replace(b"cnumpy._core.multiarray\nscalar\n", b"cnumpy.core.multiarray\nscalar\n")
+        return b.replace(b"X\x02\x00\x00\x00f8q\x03\x89\x88\x87",
+                         b"X\x02\x00\x00\x00f8q\x03K\x00K\x01\x87", 1)
 
     def next_step(self, targets=None):
         """Batch of frame dicts + target lists; contract of load_traj.py:153-224.
@@ -181,7 +228,7 @@ class DataLoader:
         for n in draw_len:
             if n == 0:
                 continue
-            entries = self.trajectories[self.frameList[draw_cols[at]]]
+            entries = self.trajectories[self.dict_data[0, draw_cols[at]]]
             at += n
             ids = [int(next(iter(e))) for e in entries]
             if len(set(ids)) == len(ids):

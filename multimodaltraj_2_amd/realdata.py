@@ -56,16 +56,18 @@ def load_raw(names, data_root):
 
 
 class SceneSource:
-    """One dataset's training split (load_traj.py:133-139): its native walk
-    index and its fp32 position / vislet rows."""
+    """One dataset as the reference's sample.py walks it: the training split's
+    bounds (load_traj.py:133-139, 163) over the frame dict the reference reads
+    (the whole CSV for the shipped datasets, load_traj.py:95-112); its native
+    walk index and the fp32 position / vislet rows of the dict's columns (the
+    vislet slice sample.py:184 reads starts at column 0, shared by both)."""
 
-    def __init__(self, name, raw_data):
+    def __init__(self, name, raw_data, frame_dict=None):
         self.name = name
-        self.loader = DataLoader(ARGS, raw_data=raw_data)
-        src = self.loader.pedsPerFrameList
+        self.loader = DataLoader(ARGS, raw_data=raw_data, frame_dict=frame_dict)
+        src = self.loader.dict_data
         self.xy = np.ascontiguousarray(np.stack([src[2], src[3]], axis=1), dtype=np.float32)
-        tr = self.loader.tr_data
-        self.vis = (np.ascontiguousarray(tr[4:6], dtype=np.float32) if tr.shape[0] >= 6 else None)
+        self.vis = (np.ascontiguousarray(src[4:6], dtype=np.float32) if src.shape[0] >= 6 else None)
         self.cols = self.xy.shape[0]
         seed, fmax = float(self.loader.seed), float(self.loader._fmax)
         self.pointers = seed + self.loader.diff * np.arange(int((fmax - seed) // self.loader.diff) + 1)
@@ -86,11 +88,16 @@ class SceneSource:
             have, self._plan = 0, None
         if count > have:
             new = self.loader.index.sample_scenes(self.pointers[have:count], nmax_cap)
-            w = max(1, int(new["n_nodes"].max(initial=0)))       # slots >= P are empty (-1)
-            new["content"] = _row_keys(self.canon[new["pos_col"][:, :, :w]],
-                                       self.canon[new["tgt_col"][:, :w]])
-            self._plan = new if self._plan is None else {
-                k: np.concatenate([self._plan[k], new[k]]) for k in new}
+            old = self._plan
+            self._plan = new if old is None else {
+                k: np.concatenate([old[k], new[k]]) for k in new if k != "content"}
+            # content keys over the WHOLE cached plan: the exact fallback of
+            # _row_keys numbers rows within one call, so keys of separate
+            # extensions must not be mixed
+            p = self._plan
+            w = max(1, int(p["n_nodes"].max(initial=0)))        # slots >= P are empty (-1)
+            p["content"] = _row_keys(self.canon[p["pos_col"][:, :, :w]],
+                                     self.canon[p["tgt_col"][:, :w]])
             self._cap = nmax_cap
         return {k: v[:count] for k, v in self._plan.items()}
 

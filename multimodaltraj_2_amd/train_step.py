@@ -99,7 +99,7 @@ class GradPlan:
         self.P = P
         self.grad = grad if grad is not None else torch.empty(P + 2, device=dev,
                                                               dtype=torch.float32)
-        self._ws = workspace(nws, dev)
+        self._ws = workspace(nws, dev, stream)
         w = params.abi()
         self._fn = lib.g2k_step_grad_f32
         self._fused = lib.g2k_step_grad_update_f32
@@ -173,7 +173,7 @@ class TrainPlan:
             _lib.check("g2k_train_workspace_bytes", -1)
         self.grad = grad if grad is not None else torch.empty(self.P + 2, device=dev,
                                                               dtype=torch.float32)
-        self._ws = workspace(nws, dev)
+        self._ws = workspace(nws, dev, stream)
         o = self.fwd.out
         w = params.abi()
         self._fn = lib.g2k_train_step_f32

@@ -107,3 +107,44 @@ def test_automatic_split_runs_the_recurrence_once(gpu):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(a.h.cpu().numpy(), o.h.cpu().numpy())
     np.testing.assert_array_equal(a.pred.cpu().numpy(), o.pred.cpu().numpy())
+
+
+def test_split_plan_on_a_side_stream_right_after_building(gpu):
+    """The workspace's first zero-fill is ordered on the plan's own stream
+    (frame_step.workspace), so a split plan launched on a side stream right
+    after it is built — no synchronize in between, as bench.py's warm-up does
+    over two streams — sees zeroed tickets: its metrics equal the same plan's
+    on the current stream, and the tickets end at zero."""
+    S, Nmax, H, F = 8, 32, 128, 20
+    b = make_batch(S, Nmax, H, F=F, seed=21)
+    t = b.to_device(gpu)
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    want = fs.step_fused(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
+                         t["h0"], split=4)
+    torch.cuda.synchronize()
+    # fill the caching allocator with non-zero blocks the workspace may reuse
+    junk = [torch.full((1 << 16,), 255, dtype=torch.uint8, device=gpu) for _ in range(8)]
+    del junk
+    side = torch.cuda.Stream(device=gpu)
+    plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
+                       split=4, stream=side)
+    for _ in range(3):
+        plan.run()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(plan.out.metrics.cpu().numpy(), want.metrics.cpu().numpy())
+    ws = plan._keep[-1]
+    assert int(ws[:64 * ((S + 15) // 16)].count_nonzero()) == 0
+    assert fs.step_split(S, F, H, Nmax, t["pos"].shape[1], b.stride) == min(4, 256 // S)
+
+
+def test_workspace_init_zero_fills_on_the_stream(gpu):
+    """g2k_workspace_init: the C caller's stream-ordered first fill."""
+    import ctypes
+    from multimodaltraj_2_amd import _lib
+    ws = torch.full((4096,), 7, dtype=torch.uint8, device=gpu)
+    s = torch.cuda.Stream(device=gpu)
+    s.wait_stream(torch.cuda.current_stream())
+    rc = _lib.load().g2k_workspace_init(ws.data_ptr(), 4096, ctypes.c_void_p(s.cuda_stream))
+    assert rc == 0
+    s.synchronize()
+    assert int(ws.count_nonzero()) == 0

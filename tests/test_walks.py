@@ -19,7 +19,7 @@ from multimodaltraj_2_amd.load_traj import DataLoader
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 ARGS = SimpleNamespace(batch_size=16, seq_length=12, pred_len=12, obs_len=8)
-NAMES = ["eth_hotel", "zara01", "zara02", "ucy_univ"]
+NAMES = ["eth_hotel", "eth_univ", "zara01", "zara02", "ucy_univ"]
 
 
 def digest(*arrays):
@@ -47,8 +47,10 @@ class Rec:
 
 
 def _loader(name):
-    raw = np.load(os.path.join(GOLDEN, f"data_{name}.npz"))["raw_data"]
-    return DataLoader(ARGS, raw_data=raw)
+    """The loader over the frame dict the reference reads for this dataset
+    (the fixture's mode: "whole" where trajectories_0.cpkl ships, else "split")."""
+    z = np.load(os.path.join(GOLDEN, f"data_{name}.npz"))
+    return DataLoader(ARGS, raw_data=z["raw_data"], frame_dict=str(z["frame_dict"]))
 
 
 def _check_targets(r, i, tgt):
@@ -142,7 +144,7 @@ def test_valid_walk_every_batch(name, tag):
 def _native_values(dl, out, j, nmax):
     """Positions / targets of scene j from the native plan (column -> CSV
     values, -1 -> the zero slot)."""
-    xy = np.stack([dl.pedsPerFrameList[2], dl.pedsPerFrameList[3]], axis=1)
+    xy = np.stack([dl.dict_data[2], dl.dict_data[3]], axis=1)
     P = min(int(out["n_nodes"][j]), nmax)
     pc = out["pos_col"][j][:, :P]                     # [8, P]
     npl = np.where(pc[..., None] >= 0, xy[np.maximum(pc, 0)], 0.0).transpose(1, 0, 2)

@@ -40,6 +40,9 @@ def per_kernel(d, counter, mode):
     return {k: sum(v) / len(v) for k, v in vals.items() if v}
 
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from multimodaltraj_2_amd.build import kernel_tree_sha  # noqa: E402
+
 mode = sys.argv[5] if len(sys.argv) > 5 else "ref"
 fetch = per_kernel(sys.argv[1], "FETCH_SIZE", mode)
 write = per_kernel(sys.argv[2], "WRITE_SIZE", mode)
@@ -50,6 +53,7 @@ res = {"config": sys.argv[3], "mode": mode,
        "fetch_size_bytes_raw": raw_f, "write_size_bytes": raw_w,
        "hbm_bytes_per_launch": 2 * raw_f + raw_w,
        "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads), WRITE_SIZE as is",
-       "per_kernel_kib": {"FETCH_SIZE": fetch, "WRITE_SIZE": write}}
+       "per_kernel_kib": {"FETCH_SIZE": fetch, "WRITE_SIZE": write},
+       "kernel_tree_sha": kernel_tree_sha()}
 json.dump(res, open(sys.argv[4], "w"), indent=1)
 print(json.dumps(res))

@@ -7,9 +7,15 @@ elsewhere).  It imports the reference's own data-side modules
 and records their outputs for the first batches of each dataset:
 
   * DataLoader.load_dataset (load_traj.py:114-150) on the dataset CSV,
-  * the frame dict of DataLoader.frame_preprocess (load_traj.py:234-256),
-    restated here because the reference only returns it through a pickle
-    file (it is rebuilt from the CSV: trajectories_0.cpkl is never unpickled),
+  * the frame dict the reference READS: DataLoader.__init__ loads
+    trajectories_0.cpkl whenever it exists (load_traj.py:95-112); each shipped
+    pickle holds frame_preprocess (load_traj.py:234-256) over the WHOLE CSV.
+    The dict is restated here over the whole CSV and checked against the
+    pickle WITHOUT unpickling it: ``pickle.dumps(dict, protocol=2)`` (as the
+    reference wrote it, :254-256, with numpy 1.x's module name and dtype
+    arguments) must equal the file's bytes.  The file's sha256 is recorded.
+    eth/univ ships no pickle: the reference builds the dict over the split
+    (:97-99), and so does the fixture,
   * DataLoader.next_step (load_traj.py:153-224) — batches and targets,
   * online_graph.ConstructGraph + get_node_attr (networkx_graph.py:30-73,
     114-150) as called by train.py:74-90 / 280-299 (float frame key cast to
@@ -41,6 +47,7 @@ OUT = os.path.join(ROOT, "tests", "golden")
 
 DATASETS = {  # name -> (dir relative to data/, csv selection index 0)
     "eth_hotel": "eth/hotel/",
+    "eth_univ": "eth/univ/",
     "zara01": "ucy/zara/zara01/",
     "zara02": "ucy/zara/zara02/",
     "ucy_univ": "ucy/univ/",
@@ -48,21 +55,52 @@ DATASETS = {  # name -> (dir relative to data/, csv selection index 0)
 N_BATCHES = 3
 
 
-def frame_dict_from_csv(dl):
-    """load_traj.py:234-256 restated (the reference writes it to a pickle)."""
-    frame_data = {i: {} for i in dl.frameList}
-    ppfl = np.transpose(dl.pedsPerFrameList)
+def frame_dict_from_csv(dl, whole):
+    """load_traj.py:234-256 restated (the reference writes it to a pickle) over
+    the whole CSV (``whole``: what the shipped pickles hold) or over the split
+    the loader holds (frameList / pedsPerFrameList, when no pickle exists)."""
+    cols = dl.raw_data if whole else dl.pedsPerFrameList
+    frames = cols[0]
+    frame_data = {i: {} for i in frames}
+    ppfl = np.transpose(cols[0:4])
     fp = dl.frame_pointer
-    while fp <= max(dl.frameList):
+    while fp <= max(frames):
         frame_data[fp] = [{ped: [px, py]} for (ind, ped, px, py) in ppfl if ind == fp]
         fp += dl.diff
     return frame_data
 
 
+def pickle_numpy1(frame_data):
+    """pickle.dump(frame_data, f, protocol=2) (load_traj.py:254-256) as numpy 1.x
+    writes it: numpy >= 2 names the scalar reducer numpy._core.multiarray and
+    passes the dtype's align/copy flags as bools (NEWFALSE/NEWTRUE) where
+    numpy 1.x wrote numpy.core.multiarray and the ints 0 / 1."""
+    import pickle
+    b = pickle.dumps(frame_data, protocol=2)
+    b = b.replace(b"cnumpy._core.multiarray\nscalar\n", b"cnumpy.core.multiarray\nscalar\n")
+    return b.replace(b"X\x02\x00\x00\x00f8q\x03\x89\x88\x87",
+                     b"X\x02\x00\x00\x00f8q\x03K\x00K\x01\x87", 1)
+
+
+def pickled_dict_check(d, frame_data):
+    """-> (mode, sha256 of trajectories_0.cpkl or ""): the pickle's bytes
+    must equal the restated whole-CSV dict's (never unpickled: a byte
+    comparison of the file with our own pickle.dumps output)."""
+    import hashlib
+    pk = os.path.join(d, "trajectories_0.cpkl")
+    if not os.path.exists(pk):
+        return "split", ""
+    raw = open(pk, "rb").read()
+    if pickle_numpy1(frame_data) != raw:
+        raise AssertionError(f"{pk}: bytes differ from the whole-CSV frame dict")
+    return "whole", hashlib.sha256(raw).hexdigest()
+
+
 def ref_loader(rel):
     """The reference's DataLoader on data/<rel> (built with __new__: its
     __init__ hard-codes /home/siri0005/..., quirk Q8), its own load_dataset,
-    and the frame dict restated from the CSV."""
+    and the frame dict it would read, restated from the CSV (whole CSV when
+    trajectories_0.cpkl exists, checked against the file's bytes)."""
     sys.path.insert(0, REF)
     import argParser
     import load_traj
@@ -76,7 +114,9 @@ def ref_loader(rel):
     dl.infer = False
     dl.current_dir = d
     dl.load_dataset(csv)
-    dl.trajectories = frame_dict_from_csv(dl)
+    whole = os.path.exists(os.path.join(d, "trajectories_0.cpkl"))
+    dl.trajectories = frame_dict_from_csv(dl, whole)
+    dl.dict_mode, dl.pickle_sha256 = pickled_dict_check(d, dl.trajectories) if whole else ("split", "")
     dl.num_batches = int((len(dl.frameList) / dl.seq_length) / dl.batch_size)
     return dl, args
 
@@ -157,7 +197,9 @@ def make_data_fixture(name, rel):
     dl.infer = False
     dl.current_dir = d
     dl.load_dataset(csv)
-    dl.trajectories = frame_dict_from_csv(dl)
+    whole = os.path.exists(os.path.join(d, "trajectories_0.cpkl"))
+    dl.trajectories = frame_dict_from_csv(dl, whole)
+    mode, sha = pickled_dict_check(d, dl.trajectories) if whole else ("split", "")
     dl.num_batches = int((len(dl.frameList) / dl.seq_length) / dl.batch_size)
     dl.reset_data_pointer()
     graph = networkx_graph.online_graph(args)
@@ -165,7 +207,9 @@ def make_data_fixture(name, rel):
     # next_step's `targets={}` default is one dict shared by every call in the
     # process (load_traj.py:153): start each dataset's fixture from empty
     load_traj.DataLoader.next_step.__defaults__[0].clear()
-    rec = {"raw_data": dl.raw_data, "num_batches": np.int64(dl.num_batches)}
+    rec = {"raw_data": dl.raw_data, "num_batches": np.int64(dl.num_batches),
+           "frame_dict": np.array(mode), "pickle_sha256": np.array(sha),
+           "dict_keys": np.int64(len(dl.trajectories))}
     frame = 1                                  # train.py:34
     for b in range(N_BATCHES):
         batch, target_traj, fptr = dl.next_step()
