@@ -179,6 +179,21 @@ int g2k_mcr_forward_f32(const g2k_dims* d, const g2k_weights* w,
                         float* pred, float lambda, void* stream);
 
 /*
+ * g2k_frame_embed_f32 — the model input of every frame alone (a2-a4).
+ * Replaces: train.py:76-85 (batch_v), 167-180 (inputs = Wii @ (batch_v @ Wi)),
+ * 182-195 (vislet_emb, vislet_rel) and the `outputs` feed of :231.
+ *   pos [S, W, Nmax, 2], vislet [S, 2, Nmax], n_active [S]; w->Wi [Nmax, D],
+ *   w->Wii [D, T] (the other weights are not read)
+ *   -> X [S, F, D+2, D] (rows 0..D-1: inputs of frame f's window rows
+ *   f*stride + t; rows D, D+1: vislet_emb), Rel [S, 2, D] = vislet_emb^2 or NULL.
+ *   D = 16.  The per-frame chain of the --use_grid_lstm encoder stage feeds
+ *   the GridLSTM output in place of rows 0..D-1 (multimodaltraj_2_amd/encoder_step.py).
+ */
+int g2k_frame_embed_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
+                        const float* vislet, const int32_t* n_active, float* X, float* Rel,
+                        void* stream);
+
+/*
  * g2k_frame_recurrence_f32 — attention + hidden-state recurrence of
  * train.py:240-252 over `frames` consecutive attention matrices.
  * Replaces: train.py:240-252 (and its copy at 622-634).

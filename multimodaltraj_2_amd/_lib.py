@@ -51,6 +51,8 @@ SYMBOLS = {
     "g2k_mcr_forward_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
                                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp]),
     "g2k_frame_recurrence_f32": (c_int, [ctypes.POINTER(G2KDims), c_vp, c_vp, c_i32, c_vp]),
+    "g2k_frame_embed_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
+                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "g2k_ade_fde_f32": (c_int, [ctypes.POINTER(G2KDims), c_vp, c_vp, c_vp, c_vp, c_vp, c_i32,
                                 c_vp, c_vp]),
     "g2k_infer_rlns_f32": (c_int, [c_vp, c_vp, c_i64, c_i32, c_vp]),

@@ -1,7 +1,7 @@
 """Flags of the reference (argParser.py:3-73), same names and defaults, plus
 the build's own: --data_root (Q8), --device, --mode,
 --world_size, --n_max, --train_batch, --train_scenes, --valid_from_seed,
---log_dir, --save_dir, --seed."""
+--log_dir, --save_dir, --seed, --use_grid_lstm."""
 import argparse
 
 
@@ -50,6 +50,10 @@ class ArgsParser:
     parser.add_argument('--valid_from_seed', type=int, default=0,
                         help="validation leg from the file's first frame (the reference starts "
                              "at frame 0, which the ETH/UCY frame keys never hit)")
+    parser.add_argument('--use_grid_lstm', type=int, default=0,
+                        help="run the vis/loc encoder's GridLSTMCell in every frame and feed its "
+                             "output as st_embeddings (train.py:201-207; 0: the reference, whose "
+                             "encoder outputs are overridden by feeds, quirk Q5)")
     parser.add_argument('--log_dir', type=str, default='log')
     parser.add_argument('--seed', type=int, default=0)
     parser.add_argument('--save_dir', type=str, default='',

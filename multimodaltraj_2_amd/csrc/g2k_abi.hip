@@ -258,6 +258,21 @@ int g2k_mcr_forward_f32(const g2k_dims* d, const g2k_weights* w, const float* X,
                             (hipStream_t)stream);
 }
 
+int g2k_frame_embed_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
+                        const float* vislet, const int32_t* n_active, float* X, float* Rel,
+                        void* stream) {
+  int rc = validate_common(d, true);
+  if (rc) return rc;
+  if (!w || !w->Wi || !w->Wii) return set_err(G2K_EINVAL, "Wi/Wii is NULL");
+  if (d->stride < 0) return set_err(G2K_EINVAL, "stride=%d < 0", d->stride);
+  if (d->F > 0 && d->W < (d->F - 1) * d->stride + kT)
+    return set_err(G2K_EINVAL, "W=%d < (F-1)*stride + T = %d", d->W, (d->F - 1) * d->stride + kT);
+  if (!pos || !vislet || !n_active || !X) return set_err(G2K_EINVAL, "a required buffer pointer is NULL");
+  if (((uintptr_t)pos & 7u) != 0) return set_err(G2K_EINVAL, "pos must be 8-byte aligned");
+  if ((int64_t)d->S * d->F == 0) return G2K_OK;
+  return embed_launch(d, w, pos, vislet, n_active, X, Rel, (hipStream_t)stream);
+}
+
 int g2k_frame_recurrence_f32(const g2k_dims* d, const float* A, float* h, int32_t frames,
                              void* stream) {
   if (!d) return set_err(G2K_EINVAL, "dims is NULL");

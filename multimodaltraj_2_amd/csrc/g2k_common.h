@@ -473,6 +473,8 @@ int recur_launch(const float* A, float* h, int S, int frames, int D, int H, hipS
 int mcr_forward_launch(const g2k_dims* d, const g2k_weights* w, const float* X, const float* Rel,
                        const float* G, const int32_t* n_active, float* A_out, float* cost_out,
                        float* pred, float lambda, hipStream_t st);
+int embed_launch(const g2k_dims* d, const g2k_weights* w, const float* pos, const float* vislet,
+                 const int32_t* n_active, float* X, float* Rel, hipStream_t st);
 int errors_launch(const g2k_dims* d, const float* pred, const float* targets,
                   const int32_t* n_active, const int32_t* n_frames, const uint8_t* ped_mask,
                   int variant, float* out, hipStream_t st);

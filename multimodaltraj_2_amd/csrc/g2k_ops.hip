@@ -171,6 +171,63 @@ __global__ void __launch_bounds__(kNT) g2k_mcr_forward_kernel(FwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// a2-a4 alone (train.py:76-85, 167-195), one workgroup per (scene, frame):
+//   B = window norms [T, n] of rows f*stride + t; X0 = Wii @ (B @ Wi) [D, D];
+//   Ve = vislet[:, :n] @ Wi [2, D]; X = [X0; Ve] (the outputs feed,
+//   train.py:231); Rel = Ve * Ve (vislet_rel, train.py:194-195; frame 0's
+//   workgroup writes it).  The model input of g2k_mcr_forward_f32, for the
+//   per-frame chain of the --use_grid_lstm encoder stage (the GridLSTM's
+//   output replaces X0 there).  D = 16.
+// ---------------------------------------------------------------------------
+struct EmbedArgs {
+  g2k_dims d;
+  g2k_weights w;
+  const float *pos, *vislet;
+  const int32_t* n_active;
+  float *X, *Rel;
+};
+
+__global__ void __launch_bounds__(kNT) g2k_embed_kernel(EmbedArgs a) {
+  __shared__ float sB[kT * kMaxN];
+  __shared__ float sU[kT * kD];
+  __shared__ float sVe[2 * kD];
+  const int F = a.d.F, Nmax = a.d.Nmax;
+  const int s = blockIdx.x / F, f = blockIdx.x - s * F, tid = threadIdx.x;
+  const int n = clampi(a.n_active[s], 0, Nmax);
+  for (int i = tid; i < kT * n; i += kNT) {        // a2: per-node L2 norm of the window rows
+    const int t = i / n, p = i - t * n;
+    const float2 xy = reinterpret_cast<const float2*>(a.pos)[((size_t)s * a.d.W + f * a.d.stride + t) * Nmax + p];
+    sB[i] = sqrtf(fmaf(xy.x, xy.x, xy.y * xy.y));
+  }
+  __syncthreads();
+  if (tid < kT * kD) {                              // U = B @ Wi
+    const int t = tid >> 4, c = tid & 15;
+    float u = 0.f;
+    for (int p = 0; p < n; ++p) u = fmaf(sB[t * n + p], a.w.Wi[p * kD + c], u);
+    sU[tid] = u;
+  } else if (tid < kT * kD + 2 * kD) {              // a4: Ve = vislet @ Wi
+    const int r = (tid - kT * kD) >> 4, c = tid & 15;
+    const float* v = a.vislet + ((size_t)s * 2 + r) * Nmax;
+    float e = 0.f;
+    for (int p = 0; p < n; ++p) e = fmaf(v[p], a.w.Wi[p * kD + c], e);
+    sVe[r * kD + c] = e;
+  }
+  __syncthreads();
+  float* X = a.X + ((size_t)s * F + f) * (kD + 2) * kD;
+  {                                                 // a3: X0 = Wii @ U (kNT == kD * kD)
+    const int i = tid >> 4, c = tid & 15;
+    float x = 0.f;
+#pragma unroll
+    for (int t = 0; t < kT; ++t) x = fmaf(a.w.Wii[i * kT + t], sU[t * kD + c], x);
+    X[tid] = x;
+  }
+  if (tid < 2 * kD) {
+    X[kD * kD + tid] = sVe[tid];
+    if (f == 0 && a.Rel) a.Rel[(size_t)s * 2 * kD + tid] = sVe[tid] * sVe[tid];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Errors from predictions: variant 0 (train.py:640-674), 1 (sample.py:21-82)
 // ---------------------------------------------------------------------------
 struct ErrArgs {
@@ -460,6 +517,15 @@ int mcr_forward_launch(const g2k_dims* d, const g2k_weights* w, const float* X, 
   a.cost_out = cost_out; a.pred = pred; a.lambda = lambda;
   hipLaunchKernelGGL(g2k_mcr_forward_kernel, dim3(d->S), dim3(kNT), 0, st, a);
   return check_launch("g2k_mcr_forward_f32");
+}
+
+int embed_launch(const g2k_dims* d, const g2k_weights* w, const float* pos, const float* vislet,
+                 const int32_t* n_active, float* X, float* Rel, hipStream_t st) {
+  static_assert(kNT == kD * kD, "one thread per X0 entry");
+  EmbedArgs a;
+  a.d = *d; a.w = *w; a.pos = pos; a.vislet = vislet; a.n_active = n_active; a.X = X; a.Rel = Rel;
+  hipLaunchKernelGGL(g2k_embed_kernel, dim3((unsigned)((int64_t)d->S * d->F)), dim3(kNT), 0, st, a);
+  return check_launch("g2k_frame_embed_f32");
 }
 
 int errors_launch(const g2k_dims* d, const float* pred, const float* targets,

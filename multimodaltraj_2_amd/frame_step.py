@@ -281,11 +281,40 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
     return lib.g2k_step_fused_f32, args, out, keep
 
 
-def mcr_forward(params: G2KParams, X, Rel, G, n_active, *, lam=LAMBDA, stream=None):
+def frame_embed(params: G2KParams, pos, vislet, n_active, F, *, stride=1, X=None, Rel=None,
+                stream=None):
+    """The model input of every frame (g2k_frame_embed_f32; train.py:76-85,
+    167-195): pos [S, W, Nmax, 2], vislet [S, 2, Nmax] -> X [S, F, D+2, D]
+    ([Wii @ (B_f @ Wi); vislet @ Wi] of frame f's window rows f*stride + t)
+    and Rel [S, 2, D] = (vislet @ Wi)^2."""
+    lib = _lib.load()
+    dev = pos.device
+    S, W, Nmax, _ = pos.shape
+    _check_dev("pos", pos, dev, torch.float32)
+    _check_dev("vislet", vislet, dev, torch.float32)
+    _check_dev("n_active", n_active, dev, torch.int32)
+    params.check(dev)
+    if tuple(vislet.shape) != (S, 2, Nmax) or params.nmax != Nmax:
+        raise ValueError("vislet must be [S, 2, Nmax] and params Nmax must match pos")
+    D = HIDDEN_LEN
+    X = X if X is not None else torch.empty((S, F, D + 2, D), device=dev, dtype=torch.float32)
+    Rel = Rel if Rel is not None else torch.empty((S, 2, D), device=dev, dtype=torch.float32)
+    if tuple(X.shape) != (S, F, D + 2, D) or tuple(Rel.shape) != (S, 2, D):
+        raise ValueError("X must be [S, F, D+2, D] and Rel [S, 2, D]")
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, D, 64, Nmax, W, stride)
+    w = params.abi()
+    rc = lib.g2k_frame_embed_f32(ctypes.byref(d), ctypes.byref(w), _ptr(pos), _ptr(vislet),
+                                 _ptr(n_active), _ptr(X), _ptr(Rel), _stream(stream))
+    _lib.check("g2k_frame_embed_f32", rc)
+    return X, Rel
+
+
+def mcr_forward(params: G2KParams, X, Rel, G, n_active, *, lam=LAMBDA, stream=None, out=None):
     """g2k_lstm_mcr.forward() for S feeds (models/g2k_lstm_mcr.py:99-124).
     X [S, D+2, D], Rel [S, 2, D], G [S, D, T] -> (attn [S,D,D], cost [S,T,T],
     pred [S, 2L, Nmax]); D = X.shape[2] in 1..16 (sample.py runs D = 10,
-    the reference checkpoints hold D = 10 weights)."""
+    the reference checkpoints hold D = 10 weights).  ``out``: (attn, cost,
+    pred) tensors of those shapes to write into (contiguous views allowed)."""
     lib = _lib.load()
     dev = X.device
     S = int(X.shape[0])
@@ -299,9 +328,17 @@ def mcr_forward(params: G2KParams, X, Rel, G, n_active, *, lam=LAMBDA, stream=No
     _check_dev("n_active", n_active, dev, torch.int32)
     for k in ("Wr", "Wc", "Wo"):
         _check_dev(k, getattr(params, k), dev, torch.float32)
-    attn = torch.empty((S, D, D), device=dev, dtype=torch.float32)
-    cost = torch.empty((S, OBS_LEN, OBS_LEN), device=dev, dtype=torch.float32)
-    pred = torch.empty((S, 2 * PRED_LEN, Nmax), device=dev, dtype=torch.float32)
+    if out is None:
+        attn = torch.empty((S, D, D), device=dev, dtype=torch.float32)
+        cost = torch.empty((S, OBS_LEN, OBS_LEN), device=dev, dtype=torch.float32)
+        pred = torch.empty((S, 2 * PRED_LEN, Nmax), device=dev, dtype=torch.float32)
+    else:
+        attn, cost, pred = out
+        for k, t, shp in (("attn", attn, (S, D, D)), ("cost", cost, (S, OBS_LEN, OBS_LEN)),
+                          ("pred", pred, (S, 2 * PRED_LEN, Nmax))):
+            if tuple(t.shape) != shp:
+                raise ValueError(f"out {k}: shape {tuple(t.shape)}, expected {shp}")
+            _check_dev(k, t, dev, torch.float32)
     d = _lib.G2KDims(S, 1, OBS_LEN, PRED_LEN, D, 64, Nmax, OBS_LEN, 0)
     w = _lib.G2KWeights(None, None, params.Wv.data_ptr(), params.bv.data_ptr(),
                         params.Wr.data_ptr(), params.Wc.data_ptr(), params.Wo.data_ptr())

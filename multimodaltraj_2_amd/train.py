@@ -30,6 +30,11 @@
   FDE (:668-674, FDE / num_nodes when the left-out dataset is 5) and their
   means, and the g2k_MPC_model_kfold_val_<l>.ckpt checkpoint (:688-693).
 
+--use_grid_lstm 1 (default 0 = the reference,
+  whose encoder outputs are overridden by feeds): both legs run the vis/loc
+  encoder's GridLSTMCell in every frame (train.py:201-207 with its output as
+  st_embeddings), one sequential chain per leg (encoder_step.EncoderChain).
+
 --mode train (the build's; the reference has no loss or optimizer): RMSProp
   (--learning_rate, --decay_rate, --grad_clip; argParser.py:38-47) on the L2
   loss of the predictions or (--loss nll) the bivariate-Gaussian NLL with a
@@ -94,10 +99,24 @@ class TrainLog:
                        np.concatenate([np.ravel(e) for e in self.euc]), delimiter=",")
 
 
-def launch_records(args, recs, loader, params, device, h, pairing):
+def encoder_cell(args, device):
+    """--use_grid_lstm: the vis/loc encoder's cell (helper.py:19-39 as
+    train.py:119-125 builds it: num_units = --num_layers, feature_size =
+    --grid_size, D / grid_size frequency blocks), seeded weights (the
+    reference's initialisers are unseeded)."""
+    from .helper import neighborhood_vis_loc_encoder
+    return neighborhood_vis_loc_encoder(hidden_size=args.rnn_size, hidden_len=fs.HIDDEN_LEN,
+                                        num_layers=args.num_layers, grid_size=args.grid_size,
+                                        embedding_size=args.embedding_size, dropout=args.dropout,
+                                        device=device, seed=args.seed).rnn
+
+
+def launch_records(args, recs, loader, params, device, h, pairing, cell=None):
     """The batches of one epoch (WalkBatch records with n >= 0) as ONE fused
     launch, then the hidden-state chain through their frames in order.
-    Returns (StepOutputs, scenes, h) with h [1, D, H] after the last frame."""
+    Returns (StepOutputs, scenes, h) with h [1, D, H] after the last frame.
+    ``cell`` (--use_grid_lstm): the encoder stage in every frame, which makes
+    the frames one sequential chain (encoder_step.EncoderChain)."""
     scs = [scene_from_record(r, loader, pairing=pairing) for r in recs]
     if not scs:
         return None, scs, h
@@ -105,6 +124,12 @@ def launch_records(args, recs, loader, params, device, h, pairing):
     S, F = len(scs), pk["F"]
     t = {k: torch.from_numpy(v).to(device) for k, v in pk.items() if isinstance(v, np.ndarray)}
     G = torch.from_numpy(context_G(args.seed, S)).to(device)
+    if cell is not None:
+        from .encoder_step import EncoderChain
+        out, h = EncoderChain(params, cell, lam=args.lambda_param).run(
+            t["pos"], t["vislet"], G, t["targets"], t["n_active"], t["n_frames"], h.contiguous(),
+            ped_mask=t["ped_mask"], stride=0)
+        return out, scs, h
     h0 = torch.zeros((S, fs.HIDDEN_LEN, args.rnn_size), device=device)
     out = fs.step_fused(params, t["pos"], t["vislet"], G, t["targets"], t["n_active"], h0,
                         n_frames=t["n_frames"], ped_mask=t["ped_mask"], stride=0,
@@ -130,6 +155,7 @@ def training_leg(args, device, params, log=print):
     counters = {"num_targets": 0, "num_end_targets": 0}              # train.py:35-36
     e_done, frame = 0, 1                                              # train.py:29, 34
     h = torch.zeros((1, fs.HIDDEN_LEN, args.rnn_size), device=device)
+    cell = encoder_cell(args, device) if getattr(args, "use_grid_lstm", 0) else None
     summary = {}
     for d in datasets:
         try:
@@ -146,16 +172,18 @@ def training_leg(args, device, params, log=print):
                 epoch.append(item)
                 continue
             ran = [r for r in epoch if r.n >= 0]
-            out, scs, h = launch_records(args, ran, loader, params, device, h, "train_log")
+            out, scs, h = launch_records(args, ran, loader, params, device, h, "train_log", cell)
             if out is not None:
                 pred = out.pred.cpu().numpy()
                 ade, fde = fs.batch_errors(out.metrics, leave_dataset=args.leaveDataset,
                                            num_nodes=[max(r.n, 1) for r in ran])
                 for s, r in enumerate(ran):
                     n = r.n
-                    if r.n_frames:
+                    if r.n_frames and cell is None:     # the frames of a batch predict alike
                         tlog.add(pred[s, 0, :, :n].reshape(2, fs.PRED_LEN, n), r.n_frames,
                                  r.target_traj)
+                    for f in range(r.n_frames if cell is not None else 0):   # they differ
+                        tlog.add(pred[s, f, :, :n].reshape(2, fs.PRED_LEN, n), 1, r.target_traj)
                     rows.append((r.index[0], r.index[1], float(ade[s]), float(fde[s]), n))
                     e, b = r.index
                     if (args.save_dir and r.outcome == "next"
@@ -196,7 +224,8 @@ def validate(args, device, params, log=print, loader=None, start_pointer=0):
         end = stop.value
     ran = [r for r in recs if r.n >= 0]                               # n = -1: the reference raises
     h = torch.zeros((1, fs.HIDDEN_LEN, args.rnn_size), device=device)   # :449
-    out, scs, h = launch_records(args, ran, loader, params, device, h, "row")
+    cell = encoder_cell(args, device) if getattr(args, "use_grid_lstm", 0) else None
+    out, scs, h = launch_records(args, ran, loader, params, device, h, "row", cell)
     cv_ade_err, cv_fde_err = [], []
     if out is not None:
         ade, fde = fs.batch_errors(out.metrics, leave_dataset=l,

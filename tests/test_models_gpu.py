@@ -157,3 +157,30 @@ def test_wc_cost_known_answer_through_hip(gpu):
 def ck_read(prefix):
     from multimodaltraj_2_amd.checkpoint import read_bundle
     return read_bundle(prefix)
+
+
+def test_attn_range_known_answer_through_hip(gpu):
+    """The 20 stored (ngh, attn) pairs of the reference's checkpoint
+    (tests/test_ckpt_kat.py): g2k_mcr_forward_f32 at D = 10 fed the stored
+    ngh (lambda = 1), E = pinv(ngh) attn and Rm = 1 returns every stored attn
+    within 1e-5 * max|attn| (normwise; |attn| ~ 0.01-0.17, so the absolute
+    1e-4 * max(1, |attn|) rule would be loose; fp32 rounding of the inputs
+    alone is ~1e-7 of it) — all 20 copies in one launch."""
+    from tests.test_ckpt_kat import _pairs, kat_feed
+    _, pairs = _pairs()
+    feeds = [kat_feed(g, A) for g, A in pairs]
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(gpu)   # noqa: E731
+    f0 = feeds[0]
+    rng = np.random.default_rng(5)
+    params = fs.G2KParams(Wi=torch.zeros((8, 10), device=gpu), Wii=torch.zeros((10, 8), device=gpu),
+                          Wv=dev(f0["Wv"]), bv=dev(f0["bv"]), Wr=dev(f0["Wr"]),
+                          Wc=dev(rng.standard_normal((24, 8))), Wo=dev(rng.standard_normal((8, 8))))
+    S = len(feeds)
+    attn, _, _ = fs.mcr_forward(params, dev(np.stack([f["X"] for f in feeds])),
+                                dev(np.stack([f["Rel"] for f in feeds])),
+                                dev(np.stack([f["G"] for f in feeds])),
+                                torch.full((S,), 8, dtype=torch.int32, device=gpu), lam=1.0)
+    torch.cuda.synchronize()
+    got = attn.cpu().numpy()
+    for i, (g, A) in enumerate(pairs):
+        assert np.abs(got[i] - A).max() <= 1e-5 * np.abs(A).max(), i

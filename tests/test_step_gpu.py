@@ -276,3 +276,25 @@ def test_step_h512_long_chain_margin(gpu):
         worst = max(worst, float(np.max(np.abs(hh[s] - h) / (np.abs(h) + 1e-3 / 512))))
         assert close_h(hh[s], h)
     print(f"H=512 F=100: max |dh| / |h| = {worst:.2e} (bound 1e-5)")
+
+
+def test_frame_embed_matches_oracle(gpu):
+    """g2k_frame_embed_f32 (a2-a4 alone) vs oracle window_norms / input_embed /
+    vislet_embed for every frame of a stride-1 window (Nmax 64, n from 1)."""
+    S, Nmax, F = 3, 64, 6
+    b = make_batch(S, Nmax, 128, F=F, seed=9, n_active=np.array([64, 1, 23], np.int32))
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    t = b.to_device(gpu)
+    X, Rel = fs.frame_embed(params, t["pos"], t["vislet"], t["n_active"], F, stride=1)
+    torch.cuda.synchronize()
+    X, Rel = X.cpu().numpy(), Rel.cpu().numpy()
+    w = params.numpy()
+    for s in range(S):
+        n = int(b.n_active[s])
+        Wi = w["Wi"][:n].astype(np.float64)
+        Ve, R = ref.vislet_embed(b.vislet[s][:, :n].astype(np.float64), Wi)
+        assert close(Rel[s], R) <= TOL
+        for f in range(F):
+            Bv = ref.window_norms(b.pos[s][f:f + 8, :n].astype(np.float64))
+            X0 = ref.input_embed(Bv, Wi, w["Wii"].astype(np.float64))
+            assert close(X[s, f], np.concatenate((X0, Ve), axis=0)) <= TOL

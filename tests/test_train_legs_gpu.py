@@ -40,7 +40,7 @@ def _args(tmp_path, data_root, leave, epochs=3):
     return a
 
 
-def _oracle_record(args, loader, rec, pairing, h0):
+def _oracle_record(args, loader, rec, pairing, h0, encoder=None):
     sc = scene_from_record(rec, loader, pairing=pairing)
     pk = pack([sc], args.rnn_size, nmax=tr.NODE_SLICE_NMAX)
     w = fs.init_params(tr.NODE_SLICE_NMAX, seed=args.seed).numpy()
@@ -48,7 +48,7 @@ def _oracle_record(args, loader, rec, pairing, h0):
     n = int(pk["n_active"][0])
     return ref.scene_step(pk["pos"][0], pk["vislet"][0], G, w, pk["targets"][0], n, h0,
                           n_frames=int(pk["n_frames"][0]), stride=0, lam=args.lambda_param,
-                          ped_mask=pk["ped_mask"][0].astype(bool))
+                          ped_mask=pk["ped_mask"][0].astype(bool), encoder=encoder)
 
 
 @pytest.mark.parametrize("leave", [3, 2])
@@ -125,3 +125,45 @@ def test_train_entry_point_validates_on_a_fresh_graph(gpu, tmp_path, data_root):
     got = [s for s in logs if s.startswith("Cross-Validation")]
     assert got == [s for s in alone if s.startswith("Cross-Validation")] and len(got) == 2
     assert os.path.exists(tmp_path / "g2k_lstm_counts_3.txt")
+
+
+def test_training_leg_with_grid_lstm_encoder(gpu, tmp_path, data_root):
+    """--use_grid_lstm 1: the vis/loc encoder's GridLSTMCell in every frame
+    (train.py:201-207, its output as st_embeddings, the hidden state entering
+    the frame as its state): one sequential chain through every batch of the
+    epoch on the GPU (encoder_step.EncoderChain) == the oracle's scene_step
+    with gridlstm_cell chained in, batch after batch (h: close_h; the per-frame
+    training-log vectors, which now differ frame to frame: 1e-4).  The cell is
+    third-party (TF contrib): parity unpinned against TF (row a6)."""
+    leave = 3
+    name, d = FIRST[leave]
+    args = _args(tmp_path, data_root, leave, epochs=1)
+    args.use_grid_lstm = 1
+    params = tr.leg_params(args, gpu)
+    summary, h, _ = tr.training_leg(args, gpu, params, log=lambda s: None)
+    cell = tr.encoder_cell(args, gpu)
+    enc = dict(W=cell.W.cpu().numpy().astype(np.float64), b=cell.b.cpu().numpy().astype(np.float64),
+               peep=tuple(cell.peep.cpu().numpy().astype(np.float64)), feature_size=cell.feature_size,
+               num_units=cell.num_units)
+    loader = DataLoader(args, datasets=[0, 1, 2, 3, 4, 5], start=d, sel=0, data_root=data_root)
+    h_ref = np.zeros((16, args.rnn_size))
+    euc, fde, ran, moved = [], [], 0, 0.0
+    for rec in walks.train_walk(loader, args, args.num_epochs):
+        if isinstance(rec, str) or rec.n < 0:
+            continue
+        pr, h_ref, m, _ = _oracle_record(args, loader, rec, "train_log", h_ref, encoder=enc)
+        for f in range(rec.n_frames):
+            e_, d_ = ref.train_log_errors(pr[f], rec.target_traj)
+            euc += e_
+            fde += d_
+        if rec.n_frames > 1:
+            moved = max(moved, float(np.abs(pr[-1] - pr[0]).max()))
+        ran += 1
+    assert ran == len(summary[d]) and ran > 3
+    assert moved > 0.0                       # with the encoder, predictions follow the chain
+    assert close_h(h[0].cpu().numpy(), h_ref)
+    got_f = np.loadtxt(tmp_path / f"g2k_MPC_fde_log_kfold_{d}.csv", delimiter=",").reshape(-1, 2)
+    got_e = np.loadtxt(tmp_path / f"g2k_MPC_error_log_kfold_{d}.csv", delimiter=",")
+    assert len(fde) > 0 and got_f.shape == (len(fde), 2)
+    assert close(got_f, np.array(fde)) <= TOL
+    assert close(got_e, np.concatenate([np.ravel(x) for x in euc])) <= TOL

@@ -310,6 +310,37 @@ def make_ckpt_scope_fixture(k=289, group=1):
     return sorted(keep)
 
 
+def make_attn_range_fixture():
+    """A second known answer from the reference's checkpoint: in every model
+    copy (20) of save/g2k_mcrAttn_model_kfold_train_4_0.ckpt-79 the forward's
+    Variables are created in the order of models/g2k_lstm_mcr.py:102-122 —
+    ngh = Variable(lambda * ngh) [10, 8] (:102), then
+    attn = Variable(ngh @ (E * Rm)) [10, 10] (:105-106) — six Variables per
+    copy from Variable_1728.  Whatever E * Rm was (its placeholder defaults are
+    re-drawn per evaluation), the saved attn lies in the column space of the
+    saved ngh: attn = ngh @ M with M = pinv(ngh) @ attn.  Stores the pairs and
+    the relative residuals |attn - ngh pinv(ngh) attn| / |attn|, and for the
+    record the relations that do NOT hold (the E-like [8, 10] Variable is no
+    factor: cost != E @ ngh, attn != ngh @ E)."""
+    t = read_bundle(os.path.join(REF, "save", "g2k_mcrAttn_model_kfold_train_4_0.ckpt-79"))
+    out, res, bad_cost, bad_attn = {}, [], [], []
+    for gi in range(20):
+        base = 1728 + 6 * gi
+        g, A, E, C = (t[f"Variable_{base + i}"] for i in range(4))
+        assert g.shape == (10, 8) and A.shape == (10, 10) and E.shape == (8, 10) and C.shape == (8, 8)
+        out[f"ngh{gi}"], out[f"attn{gi}"] = g, A
+        M = np.linalg.lstsq(g, A, rcond=None)[0]
+        res.append(np.abs(A - g @ M).max() / np.abs(A).max())
+        bad_cost.append(np.abs(E @ g - C).max() / np.abs(C).max())
+        bad_attn.append(np.abs(g @ E - A).max() / np.abs(A).max())
+    out["names"] = np.array([f"Variable_{1728 + 6 * gi}/Variable_{1729 + 6 * gi}" for gi in range(20)])
+    out["residual"] = np.array(res)
+    out["cost_vs_E_ngh"] = np.array(bad_cost)
+    out["attn_vs_ngh_E"] = np.array(bad_attn)
+    np.savez_compressed(os.path.join(OUT, "ckpt_attn_range.npz"), **out)
+    return max(res), min(bad_cost), min(bad_attn)
+
+
 def make_gridlstm_fixture():
     """GridLSTMCell weights (helper.py:31-39) from the reference's own
     checkpoint save/g2k_mcr_model_val_0.ckpt-0: W_f_0_0 [8,6], B_f_0 [6] and
@@ -333,6 +364,9 @@ def main():
         print("no /root/reference here: fixtures are committed, nothing to do")
         return
     os.makedirs(OUT, exist_ok=True)
+    if "--ckpt-only" in sys.argv:
+        print("attn in range(ngh): max residual, min cost / attn mismatch:", make_attn_range_fixture())
+        return
     for name, rel in DATASETS.items():
         rec = make_data_fixture(name, rel)
         print(name, {k: np.shape(v) for k, v in rec.items() if k.startswith("b0")})
@@ -340,6 +374,7 @@ def main():
     print("checkpoint pairs (weight_c @ cost == stored Variable):", make_ckpt_fixture())
     print("gridlstm weights:", make_gridlstm_fixture())
     print("mcrAttn model copy:", make_ckpt_scope_fixture())
+    print("attn in range(ngh): max residual, min cost / attn mismatch:", make_attn_range_fixture())
 
 
 if __name__ == "__main__":
