@@ -326,6 +326,7 @@ def train_mode(args, plan, device, *, rank=0, world=1, group=None, stepper_cls=N
     steps, idx = shard_schedule(plan.S, args.train_batch, rank, world)
     stepper = (stepper_cls or HipStepper)(args, plan, idx, device, steps)
     losses = []
+    lbuf = None                  # per-step (loss, count), kept where the gradient lives
     for e in range(args.num_epochs):
         t0 = time.time()
         for k in range(steps):
@@ -335,8 +336,11 @@ def train_mode(args, plan, device, *, rank=0, world=1, group=None, stepper_cls=N
                 g = stepper.grad(k)                  # this rank's shard
                 allreduce_grad(g, group)             # ONE collective per step
                 stepper.apply(g)                     # the same update on every rank
-            gl = g[-2:].double().cpu().numpy()
-            losses.append(float(gl[0] / max(gl[1], 1.0)))
+            if lbuf is None:
+                lbuf = torch.empty((steps, 2), dtype=g.dtype, device=g.device)
+            lbuf[k].copy_(g[-2:])                    # stream-ordered: no host round trip per step
+        gl = lbuf.double().tolist()                  # ONE host read per epoch
+        losses += [float(a / max(c, 1.0)) for a, c in gl]
         if rank == 0:
             log(f"train epoch {e}: {steps} steps x {args.train_batch} scenes "
                 f"({world} rank(s)), loss/prediction {losses[-1]:.6g}, {time.time() - t0:.2f}s")

@@ -98,12 +98,43 @@ def _port():
     return p
 
 
+class HostReads:
+    """Counts host reads of tensors (cpu / numpy / item / tolist / float)
+    issued from train.train_mode itself — the entry point's loop, not the
+    stepper (the oracle stand-in computes on the host by design)."""
+
+    NAMES = ("cpu", "numpy", "item", "tolist", "__float__")
+
+    def __init__(self):
+        self.count = 0
+        self._saved = {}
+
+    def __enter__(self):
+        import sys
+        for n in self.NAMES:
+            orig = getattr(torch.Tensor, n)
+            self._saved[n] = orig
+
+            def wrap(t, *a, _orig=orig, **k):
+                f = sys._getframe(1)
+                if f.f_code.co_name == "train_mode" and f.f_code.co_filename.endswith("train.py"):
+                    self.count += 1
+                return _orig(t, *a, **k)
+            setattr(torch.Tensor, n, wrap)
+        return self
+
+    def __exit__(self, *exc):
+        for n, orig in self._saved.items():
+            setattr(torch.Tensor, n, orig)
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    params, losses = tr.train_mode(_args(), small_plan(), torch.device("cpu"), rank=rank,
-                                   world=world, stepper_cls=OracleStepper, log=lambda s: None)
-    q.put((rank, params, losses))
+    with HostReads() as reads:
+        params, losses = tr.train_mode(_args(), small_plan(), torch.device("cpu"), rank=rank,
+                                       world=world, stepper_cls=OracleStepper, log=lambda s: None)
+    q.put((rank, params, losses, reads.count))
     dist.destroy_process_group()
 
 
@@ -126,10 +157,13 @@ def test_two_rank_gloo_train_mode_matches_one_rank():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict((r, (p, l)) for r, p, l in (q.get(timeout=600) for _ in range(world)))
+    res = [q.get(timeout=600) for _ in range(world)]
+    got = {r: (p, l) for r, p, l, _ in res}
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    # the loop reads the per-step losses once per epoch, not once per step
+    assert all(n == _args().num_epochs for *_, n in res), [n for *_, n in res]
     one, one_losses = tr.train_mode(_args(), small_plan(), torch.device("cpu"),
                                     stepper_cls=OracleStepper, log=lambda s: None)
     np.testing.assert_array_equal(got[0][0], got[1][0])          # identical replicas
