@@ -550,7 +550,7 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
         params.head = torch.zeros((3, 12), device=dev)
     ts = TrainStep(params, t0["pos"], t0["vislet"], t0["G"], t0["targets"], t0["n_active"],
                    t0["h0"], n_frames=t0["n_frames"], ped_mask=t0["ped_mask"], stride=b.stride,
-                   loss=args.loss, stream=stream if world == 1 else None, **layout)
+                   loss=args.loss, stream=stream, **layout)
     for t in batches[1:]:
         ts.bind(t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
                 n_frames=t["n_frames"], ped_mask=t["ped_mask"])
@@ -560,15 +560,15 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
         last["g"] = ts.run(i % K)
 
     # one rank: one C call per step (gradient + update), replayed from a HIP
-    # graph; across ranks the all-reduce sits between two launches (eager)
+    # graph; across ranks gradient -> all-reduce -> update are enqueued on the
+    # plans' stream with no host wait (eager: the collective is not captured)
     graph = not args.no_graph and world == 1
     if graph:
         el, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream)
         kern_s = graph_event_time(gm, stream)
     else:
         el = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
-        st = stream if world == 1 else torch.cuda.current_stream()
-        kern_s = event_time(step, max(20, min(args.steps, 200)), st)
+        kern_s = event_time(step, max(20, min(args.steps, 200)), stream)
     gl = last["g"].double().cpu().numpy()
     abytes = train_algorithmic_bytes(b, H, pbytes, ts.P, layout["targets_shared"])
     achieved = abytes / kern_s / 1e9

@@ -1572,8 +1572,17 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
   publish_metrics(a, c, NP + c.wv, NP + kRecW, acc, lsum, true);
 }
 
+// Waves per SIMD the register allocation must leave room for: an 8-wave
+// workgroup (NP = 4 below H 512) is sized for two co-resident workgroups per
+// CU (4 waves per SIMD, <= 128 VGPRs), so the next launch's scenes start on a
+// CU while this launch's recurrence waves finish their chain.
+template <int TPW, int NP>
+constexpr int scene_waves_per_eu() { return NP == 4 && TPW < 8 ? 4 : 1; }
+
 template <int TPW, int NP, bool GRAD, bool PM, bool NLL>
-__global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a, SceneLayout lay) {
+__global__ void __launch_bounds__(64 * (kRecW + NP))
+__attribute__((amdgpu_waves_per_eu(scene_waves_per_eu<TPW, NP>())))
+g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   constexpr int NT = 64 * (kRecW + NP);
   constexpr int kRB = 16 * kRecW;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1690,6 +1699,13 @@ __global__ void __launch_bounds__(64 * (kRecW + NP)) g2k_scene_kernel(StepArgs a
 int scene_producers(int H, int Nmax, bool grad) {
   (void)Nmax;
   if (H >= 512) return 4;
+  if (!grad) {
+    static const int np_env = [] {             // experiment knob: G2K_SCENE_NP = 4 | 12
+      const char* e = getenv("G2K_SCENE_NP");
+      return e ? atoi(e) : 0;
+    }();
+    if (np_env == 4) return 4;
+  }
   return grad ? 8 : 12;
 }
 
@@ -1722,6 +1738,14 @@ int launch_np(const StepArgs& a, const SceneLayout& l, int NP, int tpw, hipStrea
       }
     }
   } else {
+    if (NP == 4) {
+      switch (tpw) {
+        case 1: launch_k<1, 4, false>(a, l, st); return G2K_OK;
+        case 2: launch_k<2, 4, false>(a, l, st); return G2K_OK;
+        case 4: launch_k<4, 4, false>(a, l, st); return G2K_OK;
+        default: break;
+      }
+    }
     if (NP == 12) {
       switch (tpw) {
         case 1: launch_k<1, 12, false>(a, l, st); return G2K_OK;

@@ -254,7 +254,14 @@ class TrainStep:
         kw = dict(lr=self.lr, decay=self.decay, grad_clip=self.grad_clip)
         if self.world == 1:                            # nothing to all-reduce: update in the call
             return plan.run(self.flat, self.ms, **kw)
-        g = plan.run()
-        allreduce_grad(g, self.group)
-        optimizer_update(self.flat, g, ms=self.ms, **kw)
+        # gradient -> all-reduce -> update, all enqueued on the plan's stream
+        # with no host wait between them: ProcessGroupNCCL orders its RCCL
+        # stream after the CURRENT stream and makes the current stream wait
+        # for the collective, so the collective is issued with the plan's
+        # stream made current (gloo, CPU tests: a host copy inside gloo)
+        s = self._layout["stream"] or torch.cuda.current_stream()
+        with torch.cuda.stream(s):
+            g = plan.run()
+            allreduce_grad(g, self.group)
+            optimizer_update(self.flat, g, ms=self.ms, stream=s, **kw)
         return g
