@@ -379,10 +379,13 @@ def main(argv=None):
     ap.add_argument("--split", type=int, default=0,
                     help="workgroups per scene (G2K_STEP_SPLIT; 0: automatic, enough to cover "
                          "the CUs when a rank has fewer scenes than CUs)")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=4,
                     help="reference mode: consecutive (independent) batches on this many "
-                         "streams in turn, so one launch's start overlaps the previous one's "
-                         "end (the roofline still divides by one launch's duration)")
+                         "streams in turn, so launches overlap (the roofline still divides by "
+                         "one launch's duration)")
+    ap.add_argument("--coresident", choices=("auto", "on", "off"), default="auto",
+                    help="reference mode: G2K_STEP_CORESIDENT (two 8-wave workgroups per CU "
+                         "while launches are in flight); auto = on with 2 or more streams")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from the host instead of replaying the timed steps "
                          "from a HIP graph")
@@ -432,6 +435,7 @@ def main(argv=None):
     stream = torch.cuda.Stream(device=dev)   # the plans' stream (graph capture needs a non-default one)
     layout = dict(pred_layout=args.pred_layout, targets_shared=shared, frames=F if shared else None,
                   split=args.split)
+    cores = args.coresident == "on" or (args.coresident == "auto" and args.streams >= 2)
     abytes = algorithmic_bytes(b, H, pbytes, shared)
     K = args.rotate or max(1, -(-MALL_BYTES // abytes) + 1)
     streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(max(args.streams, 1) - 1)]
@@ -457,7 +461,7 @@ def main(argv=None):
         plans.append(fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"],
                                  t["n_active"], t["h0"], n_frames=t["n_frames"],
                                  ped_mask=t["ped_mask"], stride=b.stride, out=out,
-                                 stream=streams[k % len(streams)], **layout))
+                                 stream=streams[k % len(streams)], coresident=cores, **layout))
 
     def step(i):
         plans[i % K].run()
@@ -514,7 +518,12 @@ def main(argv=None):
                        "frames_per_step": b.frames, "obs_len": 8, "pred_len": 12, "Nmax": Nmax,
                        "hidden": H, "D": 16, "parallelism": f"dp{world}",
                        "input_batches_rotated": K, "pred_layout": args.pred_layout,
-                       "targets_shared": shared, "workgroups_per_scene": fs.step_split(S, F, H, Nmax, b.pos.shape[1], b.stride, args.split),
+                       "targets_shared": shared,
+                       "workgroups_per_scene": fs.step_split(S, F, H, Nmax, b.pos.shape[1], b.stride,
+                                                             args.split, cores),
+                       "coresident": cores,
+                       "workgroups_per_cu": fs.step_coresidency(S, F, H, Nmax, b.pos.shape[1], b.stride,
+                                                                cores),
                        "streams": len(streams),
                        "launch": "host launch per step" if args.no_graph else
                                  "HIP graph of the timed steps (one replay)"},
@@ -522,7 +531,11 @@ def main(argv=None):
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc[0], "traffic_source": pmc[1],
                          "kernel": "g2k_step_fused_f32 (g2k_scene_kernel)",
-                         "kernel_us": kern_s * 1e6, "algorithmic_bytes": abytes},
+                         "kernel_us": kern_s * 1e6, "algorithmic_bytes": abytes,
+                         # the timed steps' effective rate: launches overlap (streams,
+                         # co-resident workgroups), so bytes per step / wall per step
+                         # exceeds one launch's rate above
+                         "achieved_per_step": abytes / (elapsed / args.steps) / 1e9},
             "cpu_baseline": cpu,
             "ade_fde_all_ranks": {"ADE": float(m[0] / max(m[1], 1)),
                                   "FDE_frob_per_frame": float(np.sqrt(m[2]) / max(m[5], 1))},

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define G2K_ABI_VERSION 5
+#define G2K_ABI_VERSION 6
 
 enum {
   G2K_OK = 0,
@@ -74,6 +74,16 @@ typedef struct g2k_dims {
  * instead of 1/2 the squared error; the gradient then covers the head too
  * (P = 24 Nmax + 496 + 36, the head's 36 after Wo). */
 #define G2K_STEP_LOSS_NLL 4
+/* g2k_step_fused_f32 only (the train entry points reject it): the caller keeps
+ * two or more launches in flight on separate streams (independent batches).
+ * The step is then built from 8-wave workgroups (4 recurrence + 4 producer
+ * waves, <= 128 VGPRs, at most half the CU's LDS) so that two of them share a
+ * CU: one launch's scenes run while another's recurrence chains finish.  A
+ * lone launch is slower this way (fewer producers per scene); the throughput
+ * of launches in flight is higher.  When a scene's LDS does not fit twice
+ * (e.g. Nmax 256) or H = 512 the usual geometry is used.  The automatic
+ * split (below) is 1 under this flag: the launches in flight fill the CUs. */
+#define G2K_STEP_CORESIDENT 8
 /* Workgroups per scene (bits 8..10): G2K_STEP_SPLIT(x), x in 1..4, or 0 =
  * automatic (x = min(4, CUs / S) for the current device's CU count — 256 on
  * MI355X, 256 assumed without a device — at most F: a launch of fewer scenes

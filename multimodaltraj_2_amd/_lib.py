@@ -29,6 +29,7 @@ class G2KDims(ctypes.Structure):
 STEP_PRED_PED_MAJOR = 1      # g2k_dims.flags (include/g2k_hip.h)
 STEP_TARGETS_SHARED = 2
 STEP_LOSS_NLL = 4
+STEP_CORESIDENT = 8            # forward step: two workgroups per CU, launches in flight
 STEP_SPLIT_SHIFT = 8           # G2K_STEP_SPLIT(x): workgroups per scene, 0 = automatic
 STEP_MAX_SPLIT = 4
 
@@ -91,7 +92,7 @@ SYMBOLS = {
                                      c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class G2KLibraryError(RuntimeError):

@@ -92,8 +92,8 @@ int validate_step_inputs(const g2k_dims* d, const g2k_weights* w, const float* p
                          const float* vislet, const float* G, const float* targets,
                          const int32_t* n_active, bool train = false) {
   int rc = validate_common(d, true, false,
-                           G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED |
-                               G2K_STEP_SPLIT_MASK | (train ? G2K_STEP_LOSS_NLL : 0));
+                           G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED | G2K_STEP_SPLIT_MASK |
+                               (train ? G2K_STEP_LOSS_NLL : G2K_STEP_CORESIDENT));
   if (rc) return rc;
   if ((rc = validate_weights(w, true))) return rc;
   if (d->stride < 0) return set_err(G2K_EINVAL, "stride=%d < 0", d->stride);
@@ -167,8 +167,9 @@ int g2k_abi_version(void) { return G2K_ABI_VERSION; }
 
 const char* g2k_last_error(void) { return g_err; }
 
-constexpr int kStepFlags = G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED | G2K_STEP_SPLIT_MASK;
-constexpr int kTrainFlags = kStepFlags | G2K_STEP_LOSS_NLL;
+constexpr int kLayoutFlags = G2K_STEP_PRED_PED_MAJOR | G2K_STEP_TARGETS_SHARED | G2K_STEP_SPLIT_MASK;
+constexpr int kStepFlags = kLayoutFlags | G2K_STEP_CORESIDENT;
+constexpr int kTrainFlags = kLayoutFlags | G2K_STEP_LOSS_NLL;
 
 int64_t g2k_step_lds_bytes(const g2k_dims* d) {
   if (validate_common(d, true, false, kStepFlags) != G2K_OK) return 0;
@@ -176,7 +177,7 @@ int64_t g2k_step_lds_bytes(const g2k_dims* d) {
 }
 
 int32_t g2k_step_split(const g2k_dims* d) {
-  if (validate_common(d, true, false, kTrainFlags) != G2K_OK) return -1;
+  if (validate_common(d, true, false, kTrainFlags | kStepFlags) != G2K_OK) return -1;
   return scene_split(*d);
 }
 

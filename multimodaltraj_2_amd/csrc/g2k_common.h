@@ -418,6 +418,7 @@ constexpr int kMaxSplit = 4;
 int device_cus();   // CUs of the current device (g2k_abi.hip; 256 without a device)
 inline int scene_split(const g2k_dims& d) {
   int x = (d.flags & G2K_STEP_SPLIT_MASK) >> G2K_STEP_SPLIT_SHIFT;
+  if (x == 0 && (d.flags & G2K_STEP_CORESIDENT)) x = 1;   // launches in flight fill the CUs
   if (x == 0) {
     const int cus = device_cus();
     x = d.S >= cus ? 1 : (d.S > 0 ? cus / d.S : 1);

@@ -32,6 +32,7 @@ namespace {
 
 constexpr int kSceneChunk = 32;
 constexpr int kRecW = 4;
+constexpr int64_t kCoresidentLds = 80 * 1024;   // G2K_STEP_CORESIDENT: two workgroups' LDS per CU
 // small block of weights / per-scene matrices in LDS (floats)
 constexpr int SM_WII = 0;     // [16][8]
 constexpr int SM_WV = 128;    // [8][18]
@@ -1693,20 +1694,21 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
 // 23.6 vs NP 8 25.4; eth_hotel_synth (H 128, Nmax 32) then favoured NP 8
 // (19.9 vs 20.2), but with this round's cheaper tiles its two-tile scenes are
 // producer-bound: NP 12 19.98 vs NP 8 20.75 us (rotated inputs).  So 12
-// producers (16 waves, 4 per SIMD) for the forward; H = 512 needs > 128
+// producers (16 waves, 4 per SIMD) for a lone launch; H = 512 needs > 128
 // VGPRs per wave: 4.  Train mode keeps 8 (its producers need more than the
-// 128 VGPRs per wave that 16 waves leave).
-int scene_producers(int H, int Nmax, bool grad) {
-  (void)Nmax;
+// 128 VGPRs per wave that 16 waves leave).  G2K_STEP_CORESIDENT (launches in
+// flight): 4 producers, two 8-wave workgroups per CU when the scene's LDS
+// fits twice (round 4, 400 steps over 3-4 streams: eth_hotel_synth 15.5 ->
+// 13.5 us per step, kfold4 16.4 -> 11.2, real scenes 16.5 -> 9.3; a lone
+// launch 16.0 -> 19.3 us).
+int scene_producers(const g2k_dims& d, int H, bool grad) {
   if (H >= 512) return 4;
-  if (!grad) {
-    static const int np_env = [] {             // experiment knob: G2K_SCENE_NP = 4 | 12
-      const char* e = getenv("G2K_SCENE_NP");
-      return e ? atoi(e) : 0;
-    }();
-    if (np_env == 4) return 4;
+  if (grad) return 8;
+  if (d.flags & G2K_STEP_CORESIDENT) {
+    const SceneLayout l = scene_layout(&d, 4, false);
+    if ((int64_t)l.total * 4 <= kCoresidentLds) return 4;
   }
-  return grad ? 8 : 12;
+  return 12;
 }
 
 template <int TPW, int NP, bool GRAD, bool PM>
@@ -1762,14 +1764,14 @@ int launch_np(const StepArgs& a, const SceneLayout& l, int NP, int tpw, hipStrea
 
 int64_t scene_lds_bytes(const g2k_dims* d, bool grad) {
   const int H = grad && d->H < 64 ? 64 : d->H;
-  return (int64_t)scene_layout(d, scene_producers(H, d->Nmax, grad), grad).total * 4;
+  return (int64_t)scene_layout(d, scene_producers(*d, H, grad), grad).total * 4;
 }
 
 int scene_step_launch(const StepArgs& a, hipStream_t st) {
   const bool grad = a.grad_rows != nullptr;
   // gradient only (no h_in): the recurrence waves idle, the smallest build
   const int H = a.h_in ? a.d.H : 64;
-  const int NP = scene_producers(H, a.d.Nmax, grad);
+  const int NP = scene_producers(a.d, H, grad);
   const SceneLayout l = scene_layout(&a.d, NP, grad);
   if ((int64_t)l.total * 4 > 160 * 1024)
     return set_err(G2K_ELDS, "Nmax=%d, stride=%d needs %lld bytes of LDS", a.d.Nmax, a.d.stride,

@@ -98,12 +98,15 @@ def _stream(stream):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-def step_flags(pred_layout="band", targets_shared=False, loss="l2", split=0) -> int:
+def step_flags(pred_layout="band", targets_shared=False, loss="l2", split=0,
+               coresident=False) -> int:
     """g2k_dims.flags: pred_layout "band" = pred_path_band [S, F, 2L, Nmax],
     "ped" = pedestrian-major [S, F, Nmax, L, 2]; targets_shared = one
     [S, 1, Nmax, L, 2] target set for every frame; loss (train mode) "l2" =
     1/2 the squared error, "nll" = the bivariate-Gaussian NLL (params.head);
-    split = workgroups per scene (0: automatic, G2K_STEP_SPLIT)."""
+    split = workgroups per scene (0: automatic, G2K_STEP_SPLIT); coresident
+    (forward step only) = the caller keeps launches in flight on several
+    streams: two 8-wave workgroups per CU (G2K_STEP_CORESIDENT)."""
     if pred_layout not in ("band", "ped"):
         raise ValueError(f"pred_layout {pred_layout!r}: 'band' or 'ped'")
     if loss not in ("l2", "nll"):
@@ -113,6 +116,7 @@ def step_flags(pred_layout="band", targets_shared=False, loss="l2", split=0) -> 
     return ((_lib.STEP_PRED_PED_MAJOR if pred_layout == "ped" else 0)
             | (_lib.STEP_TARGETS_SHARED if targets_shared else 0)
             | (_lib.STEP_LOSS_NLL if loss == "nll" else 0)
+            | (_lib.STEP_CORESIDENT if coresident else 0)
             | (int(split) << _lib.STEP_SPLIT_SHIFT))
 
 
@@ -137,18 +141,31 @@ class StepOutputs:
     cost: torch.Tensor | None = None   # [S, F, T, T]
 
 
-def step_lds_bytes(S, F, H, Nmax, W, stride) -> int:
+def step_lds_bytes(S, F, H, Nmax, W, stride, coresident=False) -> int:
     lib = _lib.load()
-    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride)
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride,
+                     step_flags(coresident=coresident))
     return int(lib.g2k_step_lds_bytes(ctypes.byref(d)))
 
 
-def step_split(S, F, H, Nmax, W, stride, split=0) -> int:
+CORESIDENT_LDS = 80 * 1024     # g2k_scene.hip kCoresidentLds
+
+
+def step_coresidency(S, F, H, Nmax, W, stride, coresident=False) -> int:
+    """Workgroups of one step launch a CU holds at once: 2 under
+    G2K_STEP_CORESIDENT when the 8-wave geometry applies (H < 512 and the
+    scene's LDS fits twice, include/g2k_hip.h), else 1."""
+    if not coresident or H >= 512:
+        return 1
+    return 2 if step_lds_bytes(S, F, H, Nmax, W, stride, True) <= CORESIDENT_LDS else 1
+
+
+def step_split(S, F, H, Nmax, W, stride, split=0, coresident=False) -> int:
     """Workgroups per scene the library uses (g2k_step_split: the request, or
     the automatic choice from the current device's CU count)."""
     lib = _lib.load()
     d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride,
-                     step_flags(split=split))
+                     step_flags(split=split, coresident=coresident))
     x = int(lib.g2k_step_split(ctypes.byref(d)))
     if x < 1:
         _lib.check("g2k_step_split", -1)
@@ -174,7 +191,7 @@ def workspace(nbytes, device, stream=None):
 def step_fused(params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
                ped_mask=None, stride=1, lam=LAMBDA, out: StepOutputs | None = None,
                want_attn=False, stream=None, h_out=None, pred_layout="band",
-               targets_shared=False, frames=None, split=0) -> StepOutputs:
+               targets_shared=False, frames=None, split=0, coresident=False) -> StepOutputs:
     """One pass of the per-frame body of train.py:197-276 over S scenes.
 
     pos [S, W, Nmax, 2], vislet [S, 2, Nmax], G [S, D, T],
@@ -185,7 +202,8 @@ def step_fused(params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_fra
     plan = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
                     ped_mask=ped_mask, stride=stride, lam=lam, out=out, want_attn=want_attn,
                     stream=stream, h_out=h_out, pred_layout=pred_layout,
-                    targets_shared=targets_shared, frames=frames, split=split)
+                    targets_shared=targets_shared, frames=frames, split=split,
+                    coresident=coresident)
     plan.run()
     return plan.out
 
@@ -200,10 +218,11 @@ class StepPlan:
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
                  n_frames=None, ped_mask=None, stride=1, lam=LAMBDA,
                  out: StepOutputs | None = None, want_attn=False, stream=None, h_out=None,
-                 pred_layout="band", targets_shared=False, frames=None, split=0):
+                 pred_layout="band", targets_shared=False, frames=None, split=0,
+                 coresident=False):
         self._fn, self._args, self.out, self._keep = _prepare_step(
             params, pos, vislet, G, targets, n_active, h, n_frames, ped_mask, stride, lam, out,
-            want_attn, stream, h_out, pred_layout, targets_shared, frames, split)
+            want_attn, stream, h_out, pred_layout, targets_shared, frames, split, coresident)
 
     def run(self) -> StepOutputs:
         rc = self._fn(*self._args)
@@ -223,7 +242,7 @@ def step_frames(targets, targets_shared, frames):
 
 def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_mask, stride, lam,
                   out, want_attn, stream, h_out, pred_layout="band", targets_shared=False,
-                  frames=None, split=0):
+                  frames=None, split=0, coresident=False):
     lib = _lib.load()
     dev = pos.device
     if dev.type != "cuda":
@@ -231,7 +250,7 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
     S, W, Nmax, two = pos.shape
     if two != 2:
         raise ValueError(f"pos: last dim {two}, expected 2")
-    flags = step_flags(pred_layout, targets_shared, split=split)
+    flags = step_flags(pred_layout, targets_shared, split=split, coresident=coresident)
     F = step_frames(targets, targets_shared, frames)
     H = int(h.shape[2])
     params.check(dev)

@@ -236,15 +236,18 @@ CFG = [("eth_hotel_synth", 256), ("eth_ucy_loo_kfold4", 128), ("relational_attn_
        ("dense_crowd", 128)]
 
 
+@pytest.mark.parametrize("coresident", [False, True])
 @pytest.mark.parametrize("name,S", CFG)
-def test_config_shape_matches_oracle(gpu, name, S):
+def test_config_shape_matches_oracle(gpu, name, S, coresident):
+    """coresident: G2K_STEP_CORESIDENT (8-wave workgroups, two per CU; the
+    usual geometry where the LDS does not fit twice, dense_crowd)."""
     c = CONFIGS[name]
     Nmax, H = c["Nmax"], c["H"]
     b = make_batch(S, Nmax, H, seed=1)
     params = fs.init_params(Nmax, seed=0, device=gpu)
     t = b.to_device(gpu)
     out = fs.step_fused(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
-                        t["h0"])
+                        t["h0"], coresident=coresident)
     torch.cuda.synchronize()
     pred, hh, met = out.pred.cpu().numpy(), out.h.cpu().numpy(), out.metrics.cpu().numpy()
     w = params.numpy()
@@ -298,3 +301,36 @@ def test_frame_embed_matches_oracle(gpu):
             Bv = ref.window_norms(b.pos[s][f:f + 8, :n].astype(np.float64))
             X0 = ref.input_embed(Bv, Wi, w["Wii"].astype(np.float64))
             assert close(X[s, f], np.concatenate((X0, Ve), axis=0)) <= TOL
+
+
+@pytest.mark.parametrize("name,S", [("eth_hotel_synth", 256), ("eth_ucy_loo_kfold4", 128)])
+def test_coresident_launches_in_flight(gpu, name, S):
+    """G2K_STEP_CORESIDENT launches of 8 independent batches round-robin over
+    4 streams (bench.py's timed pattern, two workgroups per CU) compute, bit
+    for bit, what each launch computes alone; pred and h are also bit-identical
+    to the one-workgroup-per-CU geometry (same per-frame arithmetic; the metric
+    sums add the producers' partials in another grouping: 1e-4)."""
+    c = CONFIGS[name]
+    Nmax, H = c["Nmax"], c["H"]
+    assert fs.step_coresidency(S, 20, H, Nmax, 27, 1, True) == 2
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(4)]
+    plans, alone = [], []
+    for k in range(8):
+        t = make_batch(S, Nmax, H, seed=10 + k).to_device(gpu)
+        args = (params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"])
+        plans.append(fs.StepPlan(*args, stream=streams[k % 4], pred_layout="ped", coresident=True))
+        alone.append(fs.step_fused(*args, pred_layout="ped", coresident=True))
+        base = fs.step_fused(*args, pred_layout="ped")
+        torch.cuda.synchronize()
+        assert torch.equal(alone[-1].pred, base.pred) and torch.equal(alone[-1].h, base.h)
+        assert close(alone[-1].metrics.cpu().numpy(), base.metrics.cpu().numpy()) <= TOL
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for p in plans:
+            p.run()
+    torch.cuda.synchronize()
+    for p, a in zip(plans, alone):
+        assert torch.equal(p.out.pred, a.pred)
+        assert torch.equal(p.out.h, a.h)
+        assert torch.equal(p.out.metrics, a.metrics)

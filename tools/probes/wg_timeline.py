@@ -1,0 +1,198 @@
+"""Workgroup timelines of the scene kernel (development probe, not product
+code): a copy of csrc with s_memtime stamps at the phase boundaries of every
+workgroup, the CU it ran on (HW_ID / XCC_ID) and the launch it belongs to,
+built into tools/ab/libg2k_timeline.so on the CPU host; on the GPU box it
+runs launches one at a time (one stream) and concurrently (round-robin over
+several streams) and prints per-launch phase times and how many workgroups
+shared a CU at once.
+
+usage: python tools/probes/wg_timeline.py --build
+       python tools/probes/wg_timeline.py CONFIG [STREAMS [SPLIT [on|off]]]   (on: G2K_STEP_CORESIDENT)"""
+import ctypes
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "tools", "ab", "libg2k_timeline.so")
+NREC = 48
+
+DEF = r"""
+__device__ unsigned g2k_tl_buf[8192 * 48];
+__device__ unsigned g2k_tl_ctr;
+#define G2K_TL(k, cond) do { if ((cond) && c.lane == 0) { \
+  const int _s = *reinterpret_cast<const int*>(c.sWi - lay.o_wi + lay.total); \
+  g2k_tl_buf[(size_t)_s * 48 + (k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
+"""
+EXPORT = r"""
+extern "C" int g2k_tl_copy(unsigned* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2k::g2k_tl_buf), (size_t)n * 4, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int g2k_tl_count(unsigned* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2k::g2k_tl_ctr), 4, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int g2k_tl_reset(void) {
+  static unsigned z = 0;
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g2k::g2k_tl_ctr), &z, 4, 0, hipMemcpyHostToDevice);
+}
+"""
+ENTRY = r"""  if (c.tid == 0) {
+    const unsigned t0 = (unsigned)__builtin_amdgcn_s_memtime();
+    const int s_ = (int)atomicAdd(&g2k_tl_ctr, 1u);
+    reinterpret_cast<int*>(smem + lay.total)[0] = s_;
+    unsigned* r = g2k_tl_buf + (size_t)s_ * 48;
+    r[0] = blockIdx.x + 1;
+    r[1] = (unsigned)((uintptr_t)a.h_out >> 8);
+    r[2] = __builtin_amdgcn_s_getreg(63492);
+    r[3] = __builtin_amdgcn_s_getreg(63508);
+    r[4] = t0;
+  }
+"""
+REPS = [
+    ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk",
+     "namespace g2k {\n" + DEF + "namespace {\n\nconstexpr int kSceneChunk"),
+    ("  s.total = o;\n  return s;", "  s.total = o + 4;\n  return s;"),
+    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+     ENTRY + "  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("  // the first frames' attention weights (E -> A -> As into the ring, the",
+     "  G2K_TL(5, c.wv == 0);\n  // the first frames' attention weights (E -> A -> As into the ring, the"),
+    ("      float4 b0, b1;\n      int f0 = read_as(",
+     "      G2K_TL(6, c.wv == 0 && fb == 0);\n      float4 b0, b1;\n      int f0 = read_as("),
+    ("  rc.store(a.h_out + (size_t)c.s * kD * H", "  G2K_TL(7, c.wv == 0);\n  rc.store(a.h_out + (size_t)c.s * kD * H"),
+    ("    // phase 2 — predictions and errors (GRAD: and the gradient)",
+     "    G2K_TL(8 + pw, fb == 0);\n    // phase 2 — predictions and errors (GRAD: and the gradient)"),
+    ("  if (NLL) nll_worker_reduce(c, pw);\n  publish_metrics(a, c, pw,",
+     "  G2K_TL(20 + pw, true);\n  if (NLL) nll_worker_reduce(c, pw);\n  publish_metrics(a, c, pw,"),
+    ("  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA outlives the workgroup\n}",
+     "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA outlives the workgroup\n"
+     "  G2K_TL(32 + c.wv, true);\n}"),
+]
+
+
+def build():
+    from multimodaltraj_2_amd import build as b
+    from concurrent.futures import ThreadPoolExecutor
+    src = os.path.join(ROOT, "multimodaltraj_2_amd", "csrc")
+    tmp = tempfile.mkdtemp(prefix="g2k_tl_")
+    for f in os.listdir(src):
+        shutil.copy(os.path.join(src, f), tmp)
+    p = os.path.join(tmp, "g2k_scene.hip")
+    s = open(p).read()
+    for a, r in REPS:
+        assert s.count(a) == 1, a[:70]
+        s = s.replace(a, r)
+    open(p, "w").write(s + EXPORT)
+
+    def comp(f):
+        o = os.path.join(tmp, os.path.splitext(f)[0] + ".o")
+        if f.endswith(".cpp"):
+            cmd = [b.CXX, *b.CXX_FLAGS, "-c", "-o", o, os.path.join(tmp, f)]
+        else:
+            cmd = [b.HIPCC, *b.flags_for(f), "-c", "-o", o, os.path.join(tmp, f)]
+        subprocess.run(cmd, check=True)
+        return o
+
+    files = sorted(f for f in os.listdir(tmp) if f.endswith((".hip", ".cpp")))
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        objs = list(ex.map(comp, files))
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    subprocess.run([b.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT, *objs], check=True)
+    shutil.rmtree(tmp, ignore_errors=True)
+    print(OUT)
+
+
+def run(config, nstreams, split=0, cores=False):
+    import torch
+    from multimodaltraj_2_amd import _lib, frame_step as fs
+    from multimodaltraj_2_amd.synthetic import CONFIGS, make_batch
+    lib = _lib.load(OUT)
+    _lib._lib = lib
+    for n in ("g2k_tl_copy", "g2k_tl_count"):
+        getattr(lib, n).argtypes = [ctypes.c_void_p] + ([ctypes.c_int] if n == "g2k_tl_copy" else [])
+    dev = torch.device("cuda", 0)
+    cfg = dict(CONFIGS[config])
+    if config in ("eth_ucy_loo_kfold4", "dense_crowd"):
+        cfg["S"] //= 8
+    S, Nmax, H = cfg["S"], cfg["Nmax"], cfg["H"]
+    b = make_batch(S, Nmax, H, F=20, seed=1)
+    base = b.to_device(dev)
+    params = fs.init_params(Nmax, seed=0).to(dev)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(nstreams)]
+    K = 3 * nstreams
+    plans = []
+    for k in range(K):
+        t = {key: (v.clone() if isinstance(v, torch.Tensor) else v) for key, v in base.items()}
+        plans.append(fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
+                                 t["h0"], n_frames=t["n_frames"], ped_mask=t["ped_mask"],
+                                 stride=b.stride, stream=streams[k % nstreams], pred_layout="ped",
+                                 split=split, coresident=cores))
+    tags = {int(p.out.h.data_ptr() >> 8) & 0xffffffff: k for k, p in enumerate(plans)}
+    for _ in range(3):
+        for p in plans:
+            p.run()
+    torch.cuda.synchronize()
+    lib.g2k_tl_reset()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(streams[0])
+    for s in streams[1:]:
+        s.wait_stream(streams[0])
+    for p in plans:
+        p.run()
+    for s in streams[1:]:
+        streams[0].wait_stream(s)
+    e1.record(streams[0])
+    torch.cuda.synchronize()
+    wall_us = e0.elapsed_time(e1) * 1e3
+    cnt = ctypes.c_uint(0)
+    lib.g2k_tl_count(ctypes.byref(cnt))
+    n = cnt.value
+    buf = (ctypes.c_uint * (n * NREC))()
+    assert lib.g2k_tl_copy(buf, n * NREC) == 0
+    r = np.frombuffer(buf, dtype=np.uint32).reshape(n, NREC).astype(np.int64)
+    t0 = r[:, 4].min()
+    rel = lambda col: (r[:, col] - t0) % (1 << 32)   # noqa: E731
+    np_ = 4 if fs.step_coresidency(S, 20, H, Nmax, b.pos.shape[1], b.stride, cores) == 2 else 12
+    start, ex = rel(4), np.max([rel(32 + w) for w in range(4 + np_)], axis=0)
+    span_cyc = ex.max() - start.min()
+    ghz = span_cyc / wall_us / 1e3
+    print(f"{config} NP={np_} split={split} streams={nstreams} launches={K} "
+          f"workgroups={n} wall {wall_us:.1f} us ({wall_us / K:.2f} per launch), clock ~{ghz:.2f} GHz")
+    launch = np.array([tags.get(int(v), -1) for v in r[:, 1]])
+    prod_end = np.max([rel(20 + p) for p in range(np_)], axis=0)
+    heads = np.max([rel(8 + p) for p in range(np_)], axis=0)
+    cols = dict(B2=rel(5), chain0=rel(6), chain_end=rel(7), heads=heads, prod_end=prod_end, exit=ex)
+    for k in range(K):
+        m = launch == k
+        if not m.any():
+            continue
+        st = start[m]
+        line = [f"launch {k:2d} (stream {k % nstreams}): wg {m.sum():3d} start {st.min() / ghz / 1e3:7.2f}-{st.max() / ghz / 1e3:7.2f} us"]
+        for name, v in cols.items():
+            d = (v[m] - st)
+            line.append(f"{name} {np.median(d):6.0f}/{d.max():6.0f}")
+        line.append(f"end {ex[m].max() / ghz / 1e3:7.2f} us")
+        print("  ".join(line))
+    # co-residency: workgroups sharing a CU (XCC_ID, HW_ID[15:8]) at the same time
+    cu = (r[:, 3] << 8) | ((r[:, 2] >> 8) & 0xff)
+    over = np.zeros(n, dtype=int)
+    order = np.argsort(cu)
+    for key in np.unique(cu):
+        idx = np.nonzero(cu == key)[0]
+        for i in idx:
+            over[i] = int(((start[idx] < ex[i]) & (ex[idx] > start[i])).sum()) - 1
+    print("distinct CUs", len(np.unique(cu)), "; workgroups overlapping another on their CU:",
+          {int(v): int((over == v).sum()) for v in np.unique(over)})
+
+
+if __name__ == "__main__":
+    if "--build" in sys.argv:
+        build()
+    else:
+        run(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1,
+            int(sys.argv[3]) if len(sys.argv) > 3 else 0, len(sys.argv) > 4 and sys.argv[4] == "on")
