@@ -1331,7 +1331,11 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     fl = ofo + c.X * i;
   };
   const brsrc tgr = scene_targets_rsrc(a, s);
-  float2 tgA[4] = {}, tgB[4] = {};
+  // forward target buffers in flight per producer: 4 with 4 producers (10
+  // tiles each at eth_hotel_synth: two loads in flight left each HBM round
+  // trip exposed), 2 with 12 (the 128-VGPR budget of 16 waves)
+  constexpr int kNB = (!GRAD && NP == 4) ? 4 : 2;
+  float2 tg[kNB][4] = {};
   auto load_item = [&](int fb, int nitems, int k, float2 (&tg)[4]) {
     const bool ok = k < nitems;
     int fl, t;
@@ -1365,11 +1369,11 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // the first tiles' targets: in flight during the heads (GRAD: one buffer
     // and the balancing stores, see grad_frames)
     if (GRAD) {
-      load_targets(tgr, Nmax, c.nact, fb, own.fo + c.X * pw, 0, pw < gend, L, q, tgA, lay.tfb);
+      load_targets(tgr, Nmax, c.nact, fb, own.fo + c.X * pw, 0, pw < gend, L, q, tg[0], lay.tfb);
       balance_stores<PM>(a);
     } else {
-      load_item(fb, nitems, 0, tgA);
-      load_item(fb, nitems, 1, tgB);
+#pragma unroll
+      for (int j = 0; j < kNB; ++j) load_item(fb, nitems, j, tg[j]);
     }
     float rm[4];
     scene_rm(lay, c, rm);
@@ -1408,7 +1412,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // phase 2 — predictions and errors (GRAD: and the gradient)
     if (GRAD) {
       grad_frames<PM, NLL>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
-                           act_bits, acc, lsum, tgA, true);
+                           act_bits, acc, lsum, tg[0], true);
       // every worker done with the chunk's frames -> its dU rows into dV
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) atomicAdd(c.sGseq, 1);
@@ -1428,12 +1432,13 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
                                     (act_bits >> t) & 1u, Nmax, c.nact, t, L, q, acc, lsum, dm,
                                     dWoT, [] {});
       };
-      for (int k = 0; k < nitems; k += 2) {
-        item(k, tgA);
-        load_item(fb, nitems, k + 2, tgA);
-        if (k + 1 < nitems) {
-          item(k + 1, tgB);
-          load_item(fb, nitems, k + 3, tgB);
+      for (int k = 0; k < nitems; k += kNB) {
+#pragma unroll
+        for (int j = 0; j < kNB; ++j) {
+          if (k + j < nitems) {
+            item(k + j, tg[j]);
+            load_item(fb, nitems, k + j + kNB, tg[j]);
+          }
         }
       }
     }

@@ -96,5 +96,10 @@ def test_flags_rejected_where_unsupported(gpu):
     rc = lib.g2k_ade_fde_f32(ctypes.byref(d), x.data_ptr(), x.data_ptr(), x.data_ptr(), None, None,
                              0, x.data_ptr(), None)
     assert rc == -4 and b"flags" in lib.g2k_last_error()
-    d.flags = 8
+    d.flags = 16                                      # no such flag
     assert lib.g2k_step_workspace_bytes(ctypes.byref(d)) == -1
+    # G2K_STEP_CORESIDENT is a forward-step option: the train entry points reject it
+    d.flags = _lib.STEP_CORESIDENT
+    assert lib.g2k_step_workspace_bytes(ctypes.byref(d)) == 0
+    assert lib.g2k_train_workspace_bytes(ctypes.byref(d)) == -1
+    assert lib.g2k_grad_size(ctypes.byref(d)) == -1

@@ -43,7 +43,7 @@ extern "C" int g2k_tl_reset(void) {
 """
 ENTRY = r"""  if (c.tid == 0) {
     const unsigned t0 = (unsigned)__builtin_amdgcn_s_memtime();
-    const int s_ = (int)atomicAdd(&g2k_tl_ctr, 1u);
+    const int s_ = (int)(atomicAdd(&g2k_tl_ctr, 1u) & 8191u);   // (wraps: warm-up launches)
     reinterpret_cast<int*>(smem + lay.total)[0] = s_;
     unsigned* r = g2k_tl_buf + (size_t)s_ * 48;
     r[0] = blockIdx.x + 1;
@@ -152,14 +152,20 @@ def run(config, nstreams, split=0, cores=False):
     cnt = ctypes.c_uint(0)
     lib.g2k_tl_count(ctypes.byref(cnt))
     n = cnt.value
+    assert n <= 8192, n
     buf = (ctypes.c_uint * (n * NREC))()
     assert lib.g2k_tl_copy(buf, n * NREC) == 0
     r = np.frombuffer(buf, dtype=np.uint32).reshape(n, NREC).astype(np.int64)
-    t0 = r[:, 4].min()
+    # s_memtime counters are per XCD (not synchronised across XCDs): times
+    # relative to the earliest start on the workgroup's own XCD
+    xcc = r[:, 3] & 0xf
+    t0 = np.zeros(n, dtype=np.int64)
+    for x in np.unique(xcc):
+        t0[xcc == x] = r[xcc == x, 4].min()
     rel = lambda col: (r[:, col] - t0) % (1 << 32)   # noqa: E731
     np_ = 4 if fs.step_coresidency(S, 20, H, Nmax, b.pos.shape[1], b.stride, cores) == 2 else 12
     start, ex = rel(4), np.max([rel(32 + w) for w in range(4 + np_)], axis=0)
-    span_cyc = ex.max() - start.min()
+    span_cyc = np.median([ex[xcc == x].max() for x in np.unique(xcc)])
     ghz = span_cyc / wall_us / 1e3
     print(f"{config} NP={np_} split={split} streams={nstreams} launches={K} "
           f"workgroups={n} wall {wall_us:.1f} us ({wall_us / K:.2f} per launch), clock ~{ghz:.2f} GHz")
