@@ -409,6 +409,15 @@ struct StepArgs {
                       // sum's last-workgroup count (g2k_train.hip), or NULL
   int* scene_ticket;  // X > 1: [S] workgroups of a scene done (zero between launches)
   float* met_part;    // X > 1: [S][X][8] the workgroups' metric partials
+  // train step, rows folded in the same launch (g2k_scene.hip fold_rows): the
+  // last fold_g workgroups to finish sum the rows in a fixed order into
+  // grad_out [P + 2] and the last of them runs the update (up.params != NULL)
+  float* grad_out;
+  int* fold_ticket;   // [2]: workgroups finished, summers finished (zero between launches)
+  int fold_g;
+  float up_lr, up_decay, up_clip;
+  float* up_params;
+  float* up_ms;
 };
 
 // Workgroups per scene of the fused step (G2K_STEP_SPLIT, include/g2k_hip.h):

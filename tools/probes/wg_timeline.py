@@ -20,14 +20,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "ab", "libg2k_timeline.so")
-NREC = 48
+NREC = 64
 
 DEF = r"""
-__device__ unsigned g2k_tl_buf[8192 * 48];
+__device__ unsigned g2k_tl_buf[8192 * 64];
 __device__ unsigned g2k_tl_ctr;
 #define G2K_TL(k, cond) do { if ((cond) && c.lane == 0) { \
   const int _s = *reinterpret_cast<const int*>(c.sWi - lay.o_wi + lay.total); \
-  g2k_tl_buf[(size_t)_s * 48 + (k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
+  g2k_tl_buf[(size_t)_s * 64 + (k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
 """
 EXPORT = r"""
 extern "C" int g2k_tl_copy(unsigned* host, int n) {
@@ -45,7 +45,7 @@ ENTRY = r"""  if (c.tid == 0) {
     const unsigned t0 = (unsigned)__builtin_amdgcn_s_memtime();
     const int s_ = (int)(atomicAdd(&g2k_tl_ctr, 1u) & 8191u);   // (wraps: warm-up launches)
     reinterpret_cast<int*>(smem + lay.total)[0] = s_;
-    unsigned* r = g2k_tl_buf + (size_t)s_ * 48;
+    unsigned* r = g2k_tl_buf + (size_t)s_ * 64;
     r[0] = blockIdx.x + 1;
     r[1] = (unsigned)((uintptr_t)a.h_out >> 8);
     r[2] = __builtin_amdgcn_s_getreg(63492);
@@ -71,7 +71,25 @@ REPS = [
     ("  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA outlives the workgroup\n}",
      "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA outlives the workgroup\n"
      "  G2K_TL(32 + c.wv, true);\n}"),
+    ("    constexpr int kHC = GRAD ? 1 : 2;",
+     "    G2K_TL(48, pw == 0 && fb == 0);\n    int g2k_hk = 0;\n    constexpr int kHC = GRAD ? 1 : 2;"),
+    ("        __builtin_amdgcn_s_setprio(0);\n        continue;\n      }",
+     "        __builtin_amdgcn_s_setprio(0);\n        G2K_TL(49 + (g2k_hk < 6 ? g2k_hk : 6), pw == 0 && fb == 0);\n"
+     "        ++g2k_hk;\n        continue;\n      }"),
+    ("        if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      }\n      __builtin_amdgcn_s_setprio(0);\n    }",
+     "        if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      }\n      __builtin_amdgcn_s_setprio(0);\n"
+     "      G2K_TL(49 + (g2k_hk < 6 ? g2k_hk : 6), pw == 0 && fb == 0);\n      ++g2k_hk;\n    }"),
 ]
+STAGE = [
+    ("  __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed\n",
+     "  __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed\n"
+     "  G2K_TL(56 + (c.wv < kRecW ? 0 : 1), (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"),
+    ("  __builtin_amdgcn_s_waitcnt(0xc07f);                           // lgkmcnt(0)\n  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2",
+     "  G2K_TL(58 + (c.wv < kRecW ? 0 : 1), (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"
+     "  __builtin_amdgcn_s_waitcnt(0xc07f);                           // lgkmcnt(0)\n  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2"),
+]
+REPS += STAGE
+FINE = {48: "heads loop entry", 49: "head 1", 50: "head 2", 51: "head 3", 52: "head 4", 53: "head 5", 54: "head 6", 55: "head 7+"}
 
 
 def build():
@@ -182,8 +200,26 @@ def run(config, nstreams, split=0, cores=False):
         for name, v in cols.items():
             d = (v[m] - st)
             line.append(f"{name} {np.median(d):6.0f}/{d.max():6.0f}")
+        pe = np.array([rel(20 + p) for p in range(np_)])[:, m]
+        pspread = pe.max(axis=0) - pe.min(axis=0)
+        line.append(f"prod spread {np.median(pspread):6.0f}/{pspread.max():6.0f}")
         line.append(f"end {ex[m].max() / ghz / 1e3:7.2f} us")
         print("  ".join(line))
+    # producer 0's heads: entry after B2 and each head's end (cycles, medians over all workgroups)
+    e48 = rel(48) - rel(5)
+    fine = [f"entry-B2 {np.median(e48):.0f}"]
+    prev = rel(48)
+    for k in range(49, 56):
+        v = rel(k)
+        ok = r[:, k] != 0
+        if ok.sum() < n // 2:
+            break
+        fine.append(f"{FINE[k]} +{np.median((v - prev)[ok]):.0f}")
+        prev = v
+    print("producer 0:", "  ".join(fine))
+    st = {"B1 rec0": rel(56) - start, "B1 prod0": rel(57) - start, "staged rec0": rel(58) - start,
+          "staged prod0": rel(59) - start, "B2 rec0": rel(5) - start, "chain0": rel(6) - start}
+    print("lead (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in st.items()))
     # co-residency: workgroups sharing a CU (XCC_ID, HW_ID[15:8]) at the same time
     cu = (r[:, 3] << 8) | ((r[:, 2] >> 8) & 0xff)
     over = np.zeros(n, dtype=int)
