@@ -1488,11 +1488,13 @@ __device__ __forceinline__ void fold_rows(const StepArgs& a, const SceneCtx& c, 
     __builtin_amdgcn_s_sleep(2);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int C = (W + G - 1) / G, c0 = g * C, nc = min(C, W - c0);
+  const int C = (W + G - 1) / G, nc = min(C, W - g * C);
   float* red = c.sY;                                    // (the tiles' scratch, free now)
-  if (nc > 0) {
-    const int slices = kThr / nc;
-    const int col = ptid % nc, sl = ptid / nc;
+  // the chunk in blocks of at most kThr columns (few workgroups, wide rows)
+  for (int cb = 0; cb < nc; cb += kThr) {
+    const int c0 = g * C + cb, ncb = min(kThr, nc - cb);
+    const int slices = kThr / ncb;
+    const int col = ptid % ncb, sl = ptid / ncb;
     float acc = 0.f;
     if (sl < slices) {
       const float* src = a.grad_rows + c0 + col;
@@ -1506,14 +1508,15 @@ __device__ __forceinline__ void fold_rows(const StepArgs& a, const SceneCtx& c, 
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc += r0 + i * slices < total ? v[i] : 0.f;
       }
-      red[sl * nc + col] = acc;
+      red[sl * ncb + col] = acc;
     }
     sync();
-    if (ptid < nc) {
+    if (ptid < ncb) {
       float v = 0.f;
-      for (int k = 0; k < slices; ++k) v += red[k * nc + ptid];
+      for (int k = 0; k < slices; ++k) v += red[k * ncb + ptid];
       store_wt(a.grad_out + c0 + ptid, v);
     }
+    sync();                                             // (red reused by the next block)
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   sync();
@@ -1645,13 +1648,13 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     const int nrh = all_heads && fb == 0 ? rec_head_frames(lay, c) : 0;
     // GRAD: frames pw, pw + NP, ...; forward: claimed in frame order, two
     // at a time (frame_head2) when the scene is not split
-    constexpr int kHC = GRAD ? 1 : 2;
-    int hq = GRAD ? pw : claim_raw(c.sClaim, kHC);
+    const int hc = (!GRAD && c.X == 1) ? 2 : 1;              // frames per claim
+    int hq = GRAD ? pw : claim_raw(c.sClaim, hc);
     for (;;) {
       const int i = GRAD ? hq : uniform(hq);
       if (i >= nh) break;
-      hq = GRAD ? hq + NP : claim_raw(c.sClaim, kHC);        // (the next claim in flight)
-      if (!GRAD && c.X == 1 && i + 1 < nh) {
+      hq = GRAD ? hq + NP : claim_raw(c.sClaim, hc);         // (the next claim in flight)
+      if (hc == 2 && i + 1 < nh) {
         const int fl0 = i, fl1 = i + 1;
         if (fl0 >= nrh && fl0 < NP + nrh) __builtin_amdgcn_s_setprio(1);   // the first round's heads
         FrameHeadOut hd[2];
