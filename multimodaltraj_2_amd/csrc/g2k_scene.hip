@@ -1530,35 +1530,9 @@ __device__ __forceinline__ void fold_rows(const StepArgs& a, const SceneCtx& c, 
   if (__builtin_amdgcn_readfirstlane(c.sFold[1]) != G - 1) return;
   // the last summer: the complete gradient, then the update
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  if (a.up_params) {
-    const int n = W - 2;
-    const float* gr = a.grad_out;
-    const float inv = 1.0f / fmaxf(__hip_atomic_load(const_cast<float*>(gr + n + 1), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT), 1.0f);
-    float ss = 0.f;
-    for (int i = ptid; i < n; i += kThr) {
-      const float v = __hip_atomic_load(const_cast<float*>(gr + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * inv;
-      ss = fmaf(v, v, ss);
-    }
-    ss = wave_sum(ss);
-    if (lane == 0) red[pw] = ss;
-    sync();
-    float tot = 0.f;
-#pragma unroll
-    for (int w = 0; w < NP; ++w) tot += red[w];
-    const float nrm = sqrtf(tot);
-    const float scale = a.up_clip > 0.f ? inv * (a.up_clip / fmaxf(nrm, a.up_clip)) : inv;
-    for (int i = ptid; i < n; i += kThr) {
-      const float gv = __hip_atomic_load(const_cast<float*>(gr + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * scale;
-      if (a.up_ms) {
-        const float m = fmaf(a.up_decay, a.up_ms[i], (1.f - a.up_decay) * gv * gv);
-        a.up_ms[i] = m;
-        a.up_params[i] -= a.up_lr * gv / sqrtf(m + 1e-10f);
-      } else {
-        a.up_params[i] = fmaf(-a.up_lr, gv, a.up_params[i]);
-      }
-    }
-  }
+  if (a.up_params)
+    opt_step<true>(a.up_params, a.up_ms, a.grad_out, W - 2, a.up_lr, a.up_decay, a.up_clip, red, pw,
+                   NP, lane, sync);
   if (ptid == 0) {
     __hip_atomic_store(a.fold_ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(a.fold_ticket + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
