@@ -271,13 +271,7 @@ int g2k_gridlstm_f32(const float* in, int64_t ld_in, const float* state, int64_t
  * g2k_grad_size: floats P in one parameter vector = 24*Nmax + 496 (+ 36 with
  *   G2K_STEP_LOSS_NLL), laid out in g2k_weights order (Wi, Wii, Wv, bv, Wr, Wc,
  *   Wo[, head]; padded shapes); -1 on invalid dims.
- * g2k_grad_workspace_bytes: device workspace g2k_step_grad_f32 needs; like
- *   every train workspace (g2k_train_workspace_bytes) it must be zero-filled
- *   before its first use, in stream order with the first launch
- *   (g2k_workspace_init), and every call leaves it zero-filled again: the
- *   per-workgroup gradient rows are summed, and the update run, by the scene
- *   kernel's last workgroups in the same launch (ABI 6), which count their
- *   arrival in it.  One workspace per stream.
+ * g2k_grad_workspace_bytes: device workspace g2k_step_grad_f32 needs.
  * g2k_step_grad_f32: grad [P + 2] = {d loss / d params summed over the S
  *   scenes (P floats), loss, count of (frame, pedestrian) pairs}, fixed
  *   reduction order (deterministic).  Inputs as g2k_step_fused_f32.  Wr's

@@ -5,8 +5,6 @@
 #include <stdarg.h>
 #include <stdio.h>
 
-#include <algorithm>
-
 #include "g2k_common.h"
 
 namespace g2k {
@@ -147,22 +145,12 @@ int train_launch(StepArgs a, float* grad, void* workspace, int64_t workspace_byt
   const int nrows = a.d.S * scene_split(a.d);
   a.grad_rows = static_cast<float*>(workspace);
   int* line = reinterpret_cast<int*>(a.grad_rows + (size_t)nrows * width);
+  a.grad_ticket = params ? line : nullptr;
   split_ws_bind(a, line + 16);
-  // the rows are summed (and the update run) by the scene kernel's last
-  // workgroups (fold_rows): summers of 16 columns each, at most a quarter of
-  // the device's CUs, so the workgroups still running always find a slot
-  // while the summers wait (also with a second train launch in flight)
-  a.grad_out = grad;
-  a.fold_ticket = line;
-  int G = (width + 15) / 16;
-  G = std::min(G, std::max(1, device_cus() / 4));
-  a.fold_g = std::max(1, std::min(G, nrows));
-  a.up_params = params;
-  a.up_ms = params ? ms : nullptr;
-  a.up_lr = lr;
-  a.up_decay = decay;
-  a.up_clip = grad_clip;
-  return scene_step_launch(a, st);
+  if ((rc = scene_step_launch(a, st))) return rc;
+  if (!params) return grad_rows_launch(a.grad_rows, nrows, width, grad, st);
+  const UpdateArgs up{params, ms, lr, decay, grad_clip, a.grad_ticket};
+  return grad_rows_launch(a.grad_rows, nrows, width, grad, st, &up);
 }
 
 }  // namespace

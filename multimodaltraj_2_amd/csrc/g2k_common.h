@@ -409,15 +409,6 @@ struct StepArgs {
                       // sum's last-workgroup count (g2k_train.hip), or NULL
   int* scene_ticket;  // X > 1: [S] workgroups of a scene done (zero between launches)
   float* met_part;    // X > 1: [S][X][8] the workgroups' metric partials
-  // train step, rows folded in the same launch (g2k_scene.hip fold_rows): the
-  // last fold_g workgroups to finish sum the rows in a fixed order into
-  // grad_out [P + 2] and the last of them runs the update (up.params != NULL)
-  float* grad_out;
-  int* fold_ticket;   // [2]: workgroups finished, summers finished (zero between launches)
-  int fold_g;
-  float up_lr, up_decay, up_clip;
-  float* up_params;
-  float* up_ms;
 };
 
 // Workgroups per scene of the fused step (G2K_STEP_SPLIT, include/g2k_hip.h):
@@ -456,57 +447,6 @@ __host__ __device__ inline int grad_params(int Nmax, bool nll = false) {
   return 24 * Nmax + 496 + (nll ? kNllHead : 0);
 }
 __host__ __device__ inline bool loss_nll(const g2k_dims& d) { return (d.flags & G2K_STEP_LOSS_NLL) != 0; }
-
-// The optimizer step (argParser.py:38-47: grad_clip, learning_rate,
-// decay_rate) over n parameters: g = grad / max(count, 1), clipped by global
-// norm (g * clip / max(||g||, clip)), then RMSProp (ms = decay ms + (1 -
-// decay) g^2; p -= lr g / sqrt(ms + 1e-10), TF RMSPropOptimizer without
-// momentum) or SGD (ms NULL).  Run by the `nwaves` waves of the calling
-// block; the squared norm is grouped as if by one 1024-thread block (entry i
-// -> virtual lane i mod 1024, 16 virtual waves summed in order), so every
-// caller — g2k_update_kernel, the gradient-row sum, the scene kernel's folded
-// tail — produces the same bits.  red: 16 floats of LDS; sync: a barrier of
-// the calling waves.  COH: the gradient was written by other workgroups of
-// the same launch (agent-scope loads after the caller's acquire).
-template <bool COH>
-__device__ __forceinline__ float opt_grad(const float* g, int i) {
-  if (COH) return __hip_atomic_load(const_cast<float*>(g + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return g[i];
-}
-__device__ __forceinline__ void opt_entry(float* __restrict__ params, float* __restrict__ ms, int i,
-                                          float g, float lr, float decay) {
-  if (ms) {
-    const float m = fmaf(decay, ms[i], (1.f - decay) * g * g);
-    ms[i] = m;
-    params[i] = params[i] - lr * g / sqrtf(m + 1e-10f);
-  } else {
-    params[i] = fmaf(-lr, g, params[i]);
-  }
-}
-template <bool COH, typename Sync>
-__device__ __forceinline__ void opt_step(float* __restrict__ params, float* __restrict__ ms,
-                                         const float* __restrict__ grad, int n, float lr,
-                                         float decay, float clip, float* red, int wave,
-                                         int nwaves, int lane, Sync sync) {
-  const float inv = 1.0f / fmaxf(opt_grad<COH>(grad, n + 1), 1.0f);
-  for (int vw = wave; vw < 16; vw += nwaves) {
-    float ss = 0.f;
-    for (int i = 64 * vw + lane; i < n; i += 1024) {
-      const float g = opt_grad<COH>(grad, i) * inv;
-      ss = fmaf(g, g, ss);
-    }
-    ss = wave_sum(ss);
-    if (lane == 0) red[vw] = ss;
-  }
-  sync();
-  float tot = 0.f;
-#pragma unroll
-  for (int w = 0; w < 16; ++w) tot += red[w];
-  const float nrm = sqrtf(tot);
-  const float scale = clip > 0.f ? inv * (clip / fmaxf(nrm, clip)) : inv;
-  for (int i = 64 * wave + lane; i < n; i += 64 * nwaves)
-    opt_entry(params, ms, i, opt_grad<COH>(grad, i) * scale, lr, decay);
-}
 
 // g2k_train.hip
 // the optimizer step folded into the gradient-row sum (run by the workgroup

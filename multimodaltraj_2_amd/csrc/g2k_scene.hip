@@ -90,7 +90,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_small = o; o += kSceneSmall;
   const int NG = NP + kRecW;                          // train: producers + recurrence waves
   s.o_y = o;     o += grad ? NG * kL2 * kYP : 0;      // dY tile scratch (train)
-  s.o_met = o;   o += (grad ? NG : fc + 1) * 8;   // train: worker rows; forward: chunk frame rows + total
+  s.o_met = o;   o += (grad ? NG : NP) * 8;
   s.o_ring = o;  o += fc * kD * kD;
   s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
   s.o_flag = o;  o += rup4(fc);                      // As ring flags (recurrence polls)
@@ -329,105 +329,6 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
   return o;
 }
 
-// Two frames' heads at once (forward producers, frames fl0, fl1 = window
-// rows w0, w1): frame_head's arithmetic, each MFMA / VALU step issued for
-// both frames back to back so that the two dependent chains (E -> A -> As,
-// then M) overlap in one wave — a head alone is a chain of ~13 dependent
-// MFMA and softmax steps that leaves the wave mostly waiting.  The weight
-// operands (K1, K2, g, bv) are shared.  want_as[p]: frame p's As is formed
-// here (else only M: a recurrence wave forms it).
-__device__ __forceinline__ void frame_head2(const float* sm, const float* sV, const float* sVG,
-                                            const int (&wrow0)[2], int wcmax, const float (&rm)[4],
-                                            float lam, float* const (&as_dst)[2],
-                                            int* const (&as_flag)[2], const int (&flag_val)[2],
-                                            float* const (&A_g)[2], float* const (&cost_g)[2],
-                                            const bool (&want_as)[2], int L, int q,
-                                            FrameHeadOut (&o)[2]) {
-  const int L7 = L & 7, Lx = L < kL ? L : 0, q2 = q < 2 ? q : 1;
-  float ka[3], bx[3], by[3], gA[4], ua[2][3], va[2][3];
-#pragma unroll
-  for (int ks = 0; ks < 3; ++ks) {
-    const int k = 4 * ks + q;
-    ka[ks] = sm[SM_K1 + L7 * kKA + k];
-    bx[ks] = sm[SM_K2 + Lx * kKA + k];
-    by[ks] = sm[SM_K2 + (kL + Lx) * kKA + k];
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      if (ks < 2) {
-        ua[p][ks] = sV[(wrow0[p] + k) * kD + L];
-        va[p][ks] = sVG[(wrow0[p] + k) * kT + L7];
-      }
-    }
-  }
-  const float ua2 = sV[(wcmax + q2) * kD + L];                                   // Ve0, Ve1 rows
-  const float va2 = sVG[(wcmax + (q < 3 ? q : 2)) * kT + L7];                    // Ve0, Ve1, bv rows
-  const float ub = sm[SM_BV + L];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) gA[ks] = sm[SM_G + L * kT + 4 * q2 + ks];
-#pragma unroll
-  for (int ks = 0; ks < 3; ++ks) {
-    ka[ks] = L < kT ? ka[ks] : 0.f;
-    bx[ks] = L < kL ? bx[ks] : 0.f;
-    by[ks] = L < kL ? by[ks] : 0.f;
-  }
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    ua[p][2] = q < 2 ? ua2 : (q == 2 ? ub : 0.f);
-    va[p][2] = q == 3 ? 0.f : va2;
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) va[p][ks] = L < kT ? va[p][ks] : 0.f;
-  }
-  f32x4 eN[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int ks = 0; ks < 3; ++ks)
-#pragma unroll
-    for (int p = 0; p < 2; ++p) eN[p] = mfma4(ka[ks], ua[p][ks], eN[p]);       // E[4q+i][L]
-  f32x4 aA[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      aA[p] = mfma4(q < 2 ? lam * gA[ks] : 0.f, eN[p][ks] * rm[ks], aA[p]);    // A[4q+i][L]
-  // M of both frames (independent of A): in flight under the softmax
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    o[p].mT0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    o[p].mT1 = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int ks = 0; ks < 3; ++ks)
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      o[p].mT0 = mfma4(va[p][ks], bx[ks], o[p].mT0);   // M[L][4q+i]       (x rows)
-      o[p].mT1 = mfma4(va[p][ks], by[ks], o[p].mT1);   // M[12+L][4q+i]    (y rows)
-    }
-#pragma unroll
-  for (int p = 0; p < 2; ++p)
-    if (want_as[p]) attn_weights(aA[p], as_dst[p], L, q);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                // As stored before its flag
-  if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      if (want_as[p]) lds_store_flag(as_flag[p], flag_val[p]);
-  }
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    if (A_g[p] && want_as[p]) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) A_g[p][(4 * q + i) * kD + L] = aA[p][i];
-    }
-    if (cost_g[p]) {
-      f32x4 cC = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 3; ++ks) cC = mfma4(ka[ks], va[p][ks], cC);   // cost[4q+i][L]
-      if (q < 2 && L < kT) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) cost_g[p][(4 * q + i) * kT + L] = cC[i];
-      }
-    }
-  }
-}
-
 // Per-workgroup context of the scene kernel (LDS carve-up, scene scalars).
 struct SceneCtx {
   float *sWi, *sWo, *sVis, *sV, *sm, *sMet, *sRing, *sMring, *sRed, *sPos, *sVG, *sY;
@@ -435,8 +336,6 @@ struct SceneCtx {
   int* sFlag;     // As ring: global frame + 1 once the frame's As is in its slot
   int* sMflag;    // M ring: global frame + 1 once the frame's M is in its slot
   int* sTicket;   // producers' metrics ticket (after the recurrence sequence words)
-  int* sClaim;    // forward: [0] head frames, [1] tile frames claimed in this chunk (zeroed at B1)
-  int* sFold;     // train fold: [0] producer sync count, [1] the workgroup's arrival ticket
   int* sGseq;     // train: [0] producers done with the chunk's frames (cumulative), [2 + t]
                   // frames added to dWo tile t (dwo_seq)
   int s, x, X, tid, lane, wv, L, q, nact, nf, ntiles, ntact;   // x: this workgroup of the scene's X
@@ -646,7 +545,6 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
   const int wcc = (cnt - 1) * a.d.stride + kT;
   __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)
   __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed
-  if (c.tid < 2) c.sClaim[c.tid] = 0;                           // this chunk's claims (used after B2)
   if (c.wv >= kRecW) {
     const int ntile = (wcc + 3 + 15) / 16;
     const int ntask = ntile + (fb == 0 ? 1 : 0);
@@ -1353,41 +1251,38 @@ __device__ __forceinline__ void nll_worker_reduce(const SceneCtx& c, int slot) {
   }
 }
 
-// Forward producers claim work from LDS counters (one lane's ds_add_rtn);
-// the raw value is made wave-uniform only where it is used, so a claim made
-// ahead of its use does not wait for its own LDS round trip.
-__device__ __forceinline__ int claim_raw(int* ctr, int n = 1) {
-  int v = 0;
-  if ((threadIdx.x & 63) == 0) v = atomicAdd(ctr, n);
-  return v;
-}
-__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// Forward: one frame's metric partials (a producer's per-lane sums over the
-// frame's tiles, in tile order) into the chunk's frame row; the rows are
-// summed in frame order (chunk_rows_sum), so the sums do not depend on which
-// producer claimed which frame.
-__device__ __forceinline__ void frame_row(const SceneCtx& c, int fl, float (&accf)[5]) {
+// Metrics (and the train loss): each worker publishes its partial sums in
+// its row of sMet, then takes a ticket (LDS atomic); the wave drawing the
+// last of `nrows` tickets sums the rows in worker order (deterministic) and
+// writes the scene's metrics row.
+__device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCtx& c, int row,
+                                                int nrows, const float (&acc)[5], float lsum,
+                                                bool grad) {
+  const int lane = c.lane;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    const float v = wave_sum(accf[k]);
-    if (c.lane == 0) c.sMet[fl * 8 + k] = v;
-    accf[k] = 0.f;
+    const float v = wave_sum(acc[k]);
+    if (lane == 0) c.sMet[row * 8 + k] = v;
   }
-}
-// lanes 0..4: the sum of the chunk's own frame rows in frame order
-__device__ __forceinline__ float chunk_rows_sum(const SceneCtx& c, const OwnFrames& own, float v) {
-  const int l8 = c.lane < 8 ? c.lane : 7;
-  for (int i = 0; i < own.n; ++i) v += c.sMet[(own.fo + c.X * i) * 8 + l8];
-  return v;
-}
-
-// The scene's (this workgroup's) metrics row from lanes 0..4 of `v` (lane 5:
-// the frame count): directly, or (split scene) through the per-scene
-// partials in the workspace, the workgroup drawing the scene's last ticket
-// summing them in workgroup order.
-__device__ __forceinline__ void finish_metrics(const StepArgs& a, const SceneCtx& c, float v) {
-  const int lane = c.lane, l8 = lane < 8 ? lane : 7;
+  if (grad) {
+    const float v = wave_sum(lsum);
+    if (lane == 0) c.sMet[row * 8 + 5] = v;
+  }
+  int ticket = 0;
+  if (lane == 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // partials before the ticket
+    ticket = atomicAdd(c.sTicket, 1);
+  }
+  ticket = __builtin_amdgcn_readfirstlane(ticket);
+  if (ticket != nrows - 1 || !a.metrics) return;
+  const int l8 = lane < 8 ? lane : 7;
+  float v = 0.f;
+  if (lane < 5) {
+    if (c.nf > 0)
+      for (int p = 0; p < nrows; ++p) v += c.sMet[p * 8 + lane];
+  } else if (lane == 5) {
+    v = (float)c.nf;
+  }
   if (a.met_part) {
     // split scene: this workgroup's row into the scene's partials (stores that
     // write through to the coherence point, completed before the ticket); the
@@ -1413,132 +1308,6 @@ __device__ __forceinline__ void finish_metrics(const StepArgs& a, const SceneCtx
   if (lane < 8) store_wt(a.metrics + (size_t)c.s * 8 + lane, v);
 }
 
-// Metrics (and the train loss): each worker publishes its partial sums in
-// its row of sMet, then takes a ticket (LDS atomic); the wave drawing the
-// last of `nrows` tickets sums the rows in worker order (deterministic) and
-// writes the scene's metrics row.
-__device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCtx& c, int row,
-                                                int nrows, const float (&acc)[5], float lsum,
-                                                bool grad) {
-  const int lane = c.lane;
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const float v = wave_sum(acc[k]);
-    if (lane == 0) c.sMet[row * 8 + k] = v;
-  }
-  if (grad) {
-    const float v = wave_sum(lsum);
-    if (lane == 0) c.sMet[row * 8 + 5] = v;
-  }
-  int ticket = 0;
-  if (lane == 0) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // partials before the ticket
-    ticket = atomicAdd(c.sTicket, 1);
-  }
-  ticket = __builtin_amdgcn_readfirstlane(ticket);
-  if (ticket != nrows - 1 || !a.metrics) return;
-  float v = 0.f;
-  if (lane < 5) {
-    if (c.nf > 0)
-      for (int p = 0; p < nrows; ++p) v += c.sMet[p * 8 + lane];
-  } else if (lane == 5) {
-    v = (float)c.nf;
-  }
-  finish_metrics(a, c, v);
-}
-
-// Train step, the gradient rows folded into the same launch: every
-// workgroup's row [W = P + 2] is stored (write-through, completed) before its
-// arrival ticket; the last G workgroups to arrive wait for the rest, then
-// summer g adds columns [g C, (g + 1) C) of ALL rows in a fixed order (row
-// slices in order, then the slices in order: deterministic, no atomics on
-// data) into grad_out, and the last summer runs the optimizer step
-// (argParser.py:38-47: global-norm clip, RMSProp or SGD) and re-arms the
-// tickets.  Replaces g2k_grad_rows_kernel's launch (~6.8 us of tail at
-// eth_hotel_synth, round 3).  Only the last G arrivals wait (G <= a quarter
-// of the CUs), so the workgroups still to arrive always find slots.
-template <int NP>
-__device__ __forceinline__ void fold_rows(const StepArgs& a, const SceneCtx& c, int W) {
-  const int pw = c.wv - kRecW, lane = c.lane, ptid = pw * 64 + lane;
-  constexpr int kThr = NP * 64;
-  int gen = 1;
-  auto sync = [&] {                                     // the NP producer waves
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) atomicAdd(c.sFold, 1);
-    poll_word(c.sFold, NP * gen++);
-  };
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's row stores completed
-  sync();
-  const int total = (int)gridDim.x, G = a.fold_g;
-  if (pw == 0) {
-    int t = 0;
-    if (lane == 0) t = __hip_atomic_fetch_add(a.fold_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t = __builtin_amdgcn_readfirstlane(t);
-    if (lane == 0) c.sFold[1] = t;
-  }
-  sync();
-  const int t = __builtin_amdgcn_readfirstlane(c.sFold[1]);
-  if (t < total - G) return;
-  const int g = t - (total - G);
-  // every row stored: the arrival count reaches `total` (bounded wait)
-  for (int it = 0; it < kPollMax; ++it) {
-    int n = 0;
-    if (lane == 0) n = __hip_atomic_load(a.fold_ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__builtin_amdgcn_readfirstlane(n) >= total) break;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int C = (W + G - 1) / G, nc = min(C, W - g * C);
-  float* red = c.sY;                                    // (the tiles' scratch, free now)
-  // the chunk in blocks of at most kThr columns (few workgroups, wide rows)
-  for (int cb = 0; cb < nc; cb += kThr) {
-    const int c0 = g * C + cb, ncb = min(kThr, nc - cb);
-    const int slices = kThr / ncb;
-    const int col = ptid % ncb, sl = ptid / ncb;
-    float acc = 0.f;
-    if (sl < slices) {
-      const float* src = a.grad_rows + c0 + col;
-      for (int r0 = sl; r0 < total; r0 += 8 * slices) {
-        float v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = r0 + i * slices;
-          v[i] = src[(size_t)(r < total ? r : total - 1) * W];
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc += r0 + i * slices < total ? v[i] : 0.f;
-      }
-      red[sl * ncb + col] = acc;
-    }
-    sync();
-    if (ptid < ncb) {
-      float v = 0.f;
-      for (int k = 0; k < slices; ++k) v += red[k * ncb + ptid];
-      store_wt(a.grad_out + c0 + ptid, v);
-    }
-    sync();                                             // (red reused by the next block)
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  sync();
-  if (pw == 0) {
-    int t2 = 0;
-    if (lane == 0) t2 = __hip_atomic_fetch_add(a.fold_ticket + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t2 = __builtin_amdgcn_readfirstlane(t2);
-    if (lane == 0) c.sFold[1] = t2;
-  }
-  sync();
-  if (__builtin_amdgcn_readfirstlane(c.sFold[1]) != G - 1) return;
-  // the last summer: the complete gradient, then the update
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  if (a.up_params)
-    opt_step<true>(a.up_params, a.up_ms, a.grad_out, W - 2, a.up_lr, a.up_decay, a.up_clip, red, pw,
-                   NP, lane, sync);
-  if (ptid == 0) {
-    __hip_atomic_store(a.fold_ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.fold_ticket + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // Role 2: the producers (waves 4..4+NP-1).
 template <int NP, bool GRAD, bool PM, bool NLL>
 __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLayout& lay,
@@ -1546,16 +1315,32 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
   const int pw = c.wv - kRecW, L = c.L, q = c.q, lane = c.lane, s = c.s, ntact = c.ntact;
   unsigned act_bits = 0;   // formed after the first staging
-  // Forward (round 4): the producers CLAIM the chunk's frames from LDS
-  // counters — the frame heads in frame order, then whole frames of
-  // prediction tiles (every tile of a claimed frame, in tile order, by the
-  // claimer) — instead of a static round-robin: a producer slowed by its
-  // SIMD's other waves no longer holds the workgroup's tail.  Each frame's
-  // metric partials go to the frame's row (frame_row) and the rows are summed
-  // in frame order, so the result does not depend on who claimed what.
-  // (GRAD: whole frames per worker, statically, grad_frames.)
+  // tile items of a chunk (forward): item j -> frame j / ntact, tile
+  // j % ntact; this producer takes items pw, pw + NP, ...  (GRAD: whole
+  // frames per worker, grad_frames)
+  // item j -> (j / ntact, j % ntact) by a reciprocal, no division per item
+  // (exact while j * ntact < 2^16; here j < 32 ntact and ntact <= 16)
+  // Split scenes: items run over the workgroup's own frames of the chunk
+  // (local frame ofo + X i for own-frame ordinal i = j / ntact).
+  const uint32_t inv = 65536u / (uint32_t)(ntact > 0 ? ntact : 1) + 1u;
+  int ofo = 0;
+  auto item_ft = [&](int k, int& fl, int& t) {
+    const int j = pw + k * NP;
+    const int i = (int)(((uint32_t)j * inv) >> 16);
+    t = j - i * ntact;
+    fl = ofo + c.X * i;
+  };
   const brsrc tgr = scene_targets_rsrc(a, s);
-  float2 tg[2][4] = {};
+  // forward target buffers in flight per producer (4 with 4 producers
+  // measured slower: 121 VGPRs, round 4 r4f)
+  constexpr int kNB = 2;
+  float2 tg[kNB][4] = {};
+  auto load_item = [&](int fb, int nitems, int k, float2 (&tg)[4]) {
+    const bool ok = k < nitems;
+    int fl, t;
+    item_ft(ok ? k : 0, fl, t);
+    load_targets(tgr, Nmax, c.nact, fb, fl, t, ok, L, q, tg, lay.tfb);
+  };
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float lsum = 0.f;
   // the first chunk's staging ahead of the chunk loop: the loop's invariant
@@ -1573,6 +1358,8 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     }
     if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
     const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
+    ofo = own.fo;
+    const int nitems = own.n * ntact > pw ? (own.n * ntact - pw + NP - 1) / NP : 0;   // forward
     // GRAD: this producer's own frames (ordinals) pw, pw + NP, ... < gend of
     // the chunk (the last R own frames of the last chunk go to the
     // recurrence waves)
@@ -1583,31 +1370,9 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     if (GRAD) {
       load_targets(tgr, Nmax, c.nact, fb, own.fo + c.X * pw, 0, pw < gend, L, q, tg[0], lay.tfb);
       balance_stores<PM>(a);
-    }
-    // forward tiles: the stream of (own-frame ordinal j, tile t) items of the
-    // frames this producer claims, two target buffers in flight; the first
-    // frame is claimed before the heads (its first two tiles' targets then
-    // fly under them) and each next frame one frame ahead (its LDS round trip
-    // off the stream)
-    f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // (unused by the forward tiles)
-    float accf[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    int* const tctr = c.sClaim + 1;
-    int jq = 0, jA = 0, tA = 0, jB = 0, tB = 0;
-    auto next_item = [&](int j, int t, int& jn, int& tn) {
-      if (t + 1 < ntact) { jn = j; tn = t + 1; return; }
-      jn = uniform(jq); tn = 0;                            // (a stream past own.n stays there:
-      if (jn < own.n) jq = claim_raw(tctr);                //  claims only grow)
-    };
-    auto ld = [&](int j, int t, float2 (&tgb)[4]) {
-      const bool ok = j < own.n;
-      load_targets(tgr, Nmax, c.nact, fb, own.fo + c.X * (ok ? j : 0), t, ok, L, q, tgb, lay.tfb);
-    };
-    if (!GRAD && ntact > 0) {
-      jA = uniform(claim_raw(tctr));
-      jq = jA < own.n ? claim_raw(tctr) : jA;            // raw (lane 0) until used
-      ld(jA, tA, tg[0]);
-      next_item(jA, tA, jB, tB);
-      ld(jB, tB, tg[1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kNB; ++j) load_item(fb, nitems, j, tg[j]);
     }
     float rm[4];
     scene_rm(lay, c, rm);
@@ -1620,44 +1385,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     const bool all_heads = a.h_in != nullptr && c.x == 0;
     const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : c.X, nh = all_heads ? cnt : own.n;
     const int nrh = all_heads && fb == 0 ? rec_head_frames(lay, c) : 0;
-    // GRAD: frames pw, pw + NP, ...; forward: claimed in frame order, two
-    // at a time (frame_head2) when the scene is not split
-    const int hc = (!GRAD && c.X == 1) ? 2 : 1;              // frames per claim
-    int hq = GRAD ? pw : claim_raw(c.sClaim, hc);
-    for (;;) {
-      const int i = GRAD ? hq : uniform(hq);
-      if (i >= nh) break;
-      hq = GRAD ? hq + NP : claim_raw(c.sClaim, hc);         // (the next claim in flight)
-      if (hc == 2 && i + 1 < nh) {
-        const int fl0 = i, fl1 = i + 1;
-        if (fl0 >= nrh && fl0 < NP + nrh) __builtin_amdgcn_s_setprio(1);   // the first round's heads
-        FrameHeadOut hd[2];
-        const int wr[2] = {fl0 * stride, fl1 * stride};
-        float* const asd[2] = {c.sRing + fl0 * kD * kD, c.sRing + fl1 * kD * kD};
-        int* const asf[2] = {c.sFlag + fl0, c.sFlag + fl1};
-        const int fv[2] = {fb + fl0 + 1, fb + fl1 + 1};
-        float* const ag[2] = {a.A_out ? a.A_out + ((size_t)s * F + fb + fl0) * kD * kD : nullptr,
-                              a.A_out ? a.A_out + ((size_t)s * F + fb + fl1) * kD * kD : nullptr};
-        float* const cg[2] = {a.cost_out ? a.cost_out + ((size_t)s * F + fb + fl0) * kT * kT : nullptr,
-                              a.cost_out ? a.cost_out + ((size_t)s * F + fb + fl1) * kT * kT : nullptr};
-        const bool wa[2] = {fl0 >= nrh, fl1 >= nrh};
-        frame_head2(c.sm, c.sV, c.sVG, wr, lay.wcmax, rm, a.lambda, asd, asf, fv, ag, cg, wa, L, q, hd);
-        if (L < kL && q < 2) {
-#pragma unroll
-          for (int p = 0; p < 2; ++p) {
-            float* m = c.sMring + (fl0 + p) * kL2 * kT;
-            *reinterpret_cast<float4*>(m + L * kT + 4 * q) = make_float4(hd[p].mT0[0], hd[p].mT0[1], hd[p].mT0[2], hd[p].mT0[3]);
-            *reinterpret_cast<float4*>(m + (kL + L) * kT + 4 * q) = make_float4(hd[p].mT1[0], hd[p].mT1[1], hd[p].mT1[2], hd[p].mT1[3]);
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) {
-          lds_store_flag(c.sMflag + fl0, fb + fl0 + 1);
-          lds_store_flag(c.sMflag + fl1, fb + fl1 + 1);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        continue;
-      }
+    for (int i = pw; i < nh; i += NP) {
       const int fl = hb + hs * i;
       const int f = fb + fl;
       const bool mine = !all_heads || c.X == 1 || f % c.X == c.x;
@@ -1689,68 +1417,36 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       if (lane == 0) atomicAdd(c.sGseq, 1);
       poll_word(c.sGseq, NP * (fb / lay.fc + 1) + R);    // the recurrence waves add R at the end
       if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)
-    } else if (ntact > 0) {
-      auto tile = [&](int j, int t, float2 (&tgb)[4]) {
-        const int fl = own.fo + c.X * j, f = fb + fl;
-        poll_flag(c.sMflag + fl, f + 1);                     // M of this frame (maybe another producer's)
+    } else {
+      f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // (unused by the forward tiles)
+      auto item = [&](int k, float2 (&tg)[4]) {
+        int fl, t;
+        item_ft(k, fl, t);
+        const int f = fb + fl;
+        poll_flag(c.sMflag + fl, f + 1);         // M of this frame (maybe another producer's)
         const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + f) * kL2 * Nmax : a.targets,
                                     a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
         f32x4 dWoT;
-        pred_tile<false, PM, false>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tgb,
-                                    (act_bits >> t) & 1u, Nmax, c.nact, t, L, q, accf, lsum, dm,
+        pred_tile<false, PM, false>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tg,
+                                    (act_bits >> t) & 1u, Nmax, c.nact, t, L, q, acc, lsum, dm,
                                     dWoT, [] {});
-        if (t == ntact - 1) frame_row(c, fl, accf);
       };
-      while (jA < own.n) {
-        tile(jA, tA, tg[0]);
-        int jC, tC;
-        next_item(jB, tB, jC, tC);
-        ld(jC, tC, tg[0]);
-        if (jB >= own.n) break;
-        tile(jB, tB, tg[1]);
-        int jD, tD;
-        next_item(jC, tC, jD, tD);
-        ld(jD, tD, tg[1]);
-        jA = jC; tA = tC; jB = jD; tB = tD;
+      for (int k = 0; k < nitems; k += kNB) {
+#pragma unroll
+        for (int j = 0; j < kNB; ++j) {
+          if (k + j < nitems) {
+            item(k + j, tg[j]);
+            load_item(fb, nitems, k + j + kNB, tg[j]);
+          }
+        }
       }
-    }
-    if (!GRAD && fb + lay.fc < c.nf) {
-      // chunk done: the first producer adds the chunk's frame rows (frame
-      // order) to the running total row after B3, before the next chunk's
-      // staging barrier, so no row is rewritten under it
-      __syncthreads();                                          // B3
-      if (pw == 0 && ntact > 0) {
-        float* tot = c.sMet + lay.fc * 8;
-        const float v = chunk_rows_sum(c, own, fb > 0 ? tot[lane < 8 ? lane : 7] : 0.f);
-        if (lane < 5) tot[lane] = v;
-      }
-      continue;
     }
     if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
   }
-  if (!GRAD) {
-    // forward metrics: every producer's frame rows stored, then a ticket; the
-    // producer drawing the last sums the running total and the last chunk's
-    // rows in frame order
-    int ticket = 0;
-    if (lane == 0) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      ticket = atomicAdd(c.sTicket, 1);
-    }
-    if (uniform(ticket) != NP - 1 || !a.metrics) return;
-    float v = 0.f;
-    if (c.nf > 0 && ntact > 0) {
-      const int fb = ((c.nf - 1) / lay.fc) * lay.fc;
-      const OwnFrames own = own_frames(fb, c.nf - fb, c.X, c.x);
-      v = chunk_rows_sum(c, own, fb > 0 ? c.sMet[lay.fc * 8 + (lane < 8 ? lane : 7)] : 0.f);
-    }
-    if (lane >= 5) v = lane == 5 ? (float)c.nf : 0.f;
-    finish_metrics(a, c, v);
-    return;
-  }
-  // metrics and the loss: also the recurrence waves' rows (NP + w)
+  // metrics (and the loss): GRAD also the recurrence waves' rows (NP + w)
   if (NLL) nll_worker_reduce(c, pw);
-  publish_metrics(a, c, pw, NP + kRecW, acc, lsum, GRAD);
+  publish_metrics(a, c, pw, GRAD ? NP + kRecW : NP, acc, lsum, GRAD);
+  if (!GRAD) return;
   // GRAD: every producer has added its frames once the ticket count is NP;
   // then the scene's gradient row [P + 2] (g2k_weights order) is formed by
   // all producers together
@@ -1852,7 +1548,6 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     }
     store_wt(row + p, x);
   }
-  if (a.grad_out) fold_rows<NP>(a, c, P + 2);
 }
 
 // GRAD, recurrence wave w after its recurrence: the last R frames of the
@@ -1917,8 +1612,6 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   c.sMflag = reinterpret_cast<int*>(smem + lay.o_mflag);
   c.sY = smem + lay.o_y;
   c.sTicket = reinterpret_cast<int*>(c.sRed + 2 * kRB) + kRecW;
-  c.sClaim = c.sTicket + 1;
-  c.sFold = c.sTicket + 3;
   c.sCost = smem + lay.o_cost; c.sGFrame = smem + lay.o_gframe;
   c.sGPriv = smem + lay.o_gpriv; c.sGPdV = smem + lay.o_gpdv;
   c.sGAcc = smem + lay.o_gacc;
@@ -1926,7 +1619,7 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   c.sGseq = reinterpret_cast<int*>(smem + lay.o_gseq);
   c.sNllA = smem + lay.o_nlla; c.sNllW = smem + lay.o_nllw;
   c.sNllR = smem + lay.o_nllr; c.sNllC = smem + lay.o_nllc;
-  if (c.tid < 8) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket, claims, fold
+  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket
   if (GRAD) {                                          // accumulators and their sequence words
     for (int i = c.tid; i < lay.o_gseq + rup4(2 + c.ntiles) - lay.o_gacc; i += NT) smem[lay.o_gacc + i] = 0.f;
     if (a.grad_ticket && blockIdx.x == 0 && c.tid == 0) *a.grad_ticket = 0;   // this step's update ticket

@@ -8,12 +8,116 @@
 namespace g2k {
 namespace {
 
+// Optimizer step (argParser.py:38-47: grad_clip, learning_rate, decay_rate):
+// g = grad / count, clipped by global norm (g * clip / max(||g||, clip)),
+// then RMSProp (ms = decay ms + (1 - decay) g^2; p -= lr g / sqrt(ms +
+// 1e-10), TF RMSPropOptimizer without momentum) or SGD (ms NULL).  One
+// workgroup of 1024: the norm is a fixed-order block reduction.  COH: the
+// gradient is read with agent-scope atomic loads (it was just written by
+// other workgroups of the same launch, see g2k_grad_rows_kernel).
+template <bool COH>
+__device__ __forceinline__ float grad_at(const float* g, int i) {
+  if (COH) return __hip_atomic_load(const_cast<float*>(g + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return g[i];
+}
+
+constexpr int kPre = 8;   // entries per thread held in registers (n <= 8192)
+
+// this thread's parameters and mean squares (entries tid + 1024 j), loaded
+// ahead of the gradient they are updated with
+__device__ __forceinline__ void load_update_state(const float* __restrict__ params,
+                                                  const float* __restrict__ ms, int n,
+                                                  float (&pp)[kPre], float (&pm)[kPre]) {
+#pragma unroll
+  for (int j = 0; j < kPre; ++j) {
+    const int i = threadIdx.x + j * 1024;
+    pp[j] = i < n ? params[i] : 0.f;
+    pm[j] = (ms && i < n) ? ms[i] : 0.f;
+  }
+}
+
+// PRE: pp / pm already hold this thread's parameters and mean squares
+// (load_update_state; n <= kPre * 1024)
+template <bool COH, bool PRE = false>
+__device__ __forceinline__ void update_body(float* __restrict__ params, float* __restrict__ ms,
+                                            const float* __restrict__ grad, int n, float lr,
+                                            float decay, float clip, float* red,
+                                            float (*ppre)[kPre] = nullptr,
+                                            float (*pmre)[kPre] = nullptr) {
+  const int tid = threadIdx.x;
+  // up to kPre entries per thread: parameters and mean squares are loaded
+  // together with the gradient, before the norm's reduction
+  const bool pre = n <= kPre * 1024;
+  float pg[kPre], pp[kPre], pm[kPre];
+  if (pre) {
+    if (PRE) {
+#pragma unroll
+      for (int j = 0; j < kPre; ++j) { pp[j] = (*ppre)[j]; pm[j] = (*pmre)[j]; }
+    } else {
+      load_update_state(params, ms, n, pp, pm);
+    }
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int i = tid + j * 1024;
+      pg[j] = i < n ? grad_at<COH>(grad, i) : 0.f;
+    }
+  }
+  const float inv = 1.0f / fmaxf(grad_at<COH>(grad, n + 1), 1.0f);
+  float ss = 0.f;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const float g = pg[j] * inv;
+      ss = fmaf(g, g, ss);
+    }
+  } else {
+    for (int i = tid; i < n; i += 1024) {
+      const float g = grad_at<COH>(grad, i) * inv;
+      ss = fmaf(g, g, ss);
+    }
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) tot += red[w];
+  const float nrm = sqrtf(tot);
+  const float scale = clip > 0.f ? inv * (clip / fmaxf(nrm, clip)) : inv;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int i = tid + j * 1024;
+      if (i >= n) break;
+      const float g = pg[j] * scale;
+      if (ms) {
+        const float m = fmaf(decay, pm[j], (1.f - decay) * g * g);
+        ms[i] = m;
+        params[i] = pp[j] - lr * g / sqrtf(m + 1e-10f);
+      } else {
+        params[i] = fmaf(-lr, g, pp[j]);
+      }
+    }
+    return;
+  }
+  for (int i = tid; i < n; i += 1024) {
+    const float g = grad_at<COH>(grad, i) * scale;
+    if (ms) {
+      const float m = fmaf(decay, ms[i], (1.f - decay) * g * g);
+      ms[i] = m;
+      params[i] -= lr * g / sqrtf(m + 1e-10f);
+    } else {
+      params[i] = fmaf(-lr, g, params[i]);
+    }
+  }
+}
+
 // grad[p] = sum_s rows[s][p]: workgroup = 32 columns x 32 row slices; slice
 // k sums rows k, k + 32, ... in order with eight loads in flight (the rows
 // one thread adds — 8 of the usual 256 — come in ONE memory round trip),
 // then the 32 slices in order (the same sum for every launch: deterministic,
 // no atomics on data).  UPD: the workgroup that finishes last then runs the
-// optimizer step (opt_step) on the complete gradient.
+// optimizer step on the complete gradient (one launch fewer per train step).
 // The hand-off uses agent-scope atomics only — gradient stores that write
 // through to the coherence point (sc1), their completion (vmcnt(0)) before
 // the ticket's fetch-add, coherent loads by the last workgroup — so no L2
@@ -29,6 +133,11 @@ __global__ void __launch_bounds__(kRowCols * kRowSlices) g2k_grad_rows_kernel(co
   __shared__ int last;
   const int c = threadIdx.x % kRowCols, sl = threadIdx.x / kRowCols;
   const int p = blockIdx.x * kRowCols + c;
+  // UPD: the update's parameters and mean squares in flight with the rows
+  // (only the last workgroup uses them: one memory round trip off its tail)
+  float pp[kPre], pm[kPre];
+  const bool pre = UPD && width - 2 <= kPre * 1024;
+  if (pre) load_update_state(up.params, up.ms, width - 2, pp, pm);
   float acc = 0.f;
   if (p < width) {
     for (int r0 = sl; r0 < S; r0 += 8 * kRowSlices) {
@@ -64,8 +173,11 @@ __global__ void __launch_bounds__(kRowCols * kRowSlices) g2k_grad_rows_kernel(co
   // under the HIP memory model, not just by gfx950's store ordering (their
   // write-through stores completed, vmcnt(0), before their ticket increments)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  opt_step<true>(up.params, up.ms, grad, width - 2, up.lr, up.decay, up.clip, &red[0][0],
-                 wave_id(), 16, threadIdx.x & 63, [] { __syncthreads(); });
+  if (pre)
+    update_body<true, true>(up.params, up.ms, grad, width - 2, up.lr, up.decay, up.clip, &red[0][0],
+                            &pp, &pm);
+  else
+    update_body<true>(up.params, up.ms, grad, width - 2, up.lr, up.decay, up.clip, &red[0][0]);
 }
 
 __global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ params,
@@ -73,8 +185,7 @@ __global__ void __launch_bounds__(1024) g2k_update_kernel(float* __restrict__ pa
                                                           const float* __restrict__ grad, int n,
                                                           float lr, float decay, float clip) {
   __shared__ float red[16];
-  opt_step<false>(params, ms, grad, n, lr, decay, clip, red, wave_id(), 16, threadIdx.x & 63,
-                  [] { __syncthreads(); });
+  update_body<false>(params, ms, grad, n, lr, decay, clip, red);
 }
 
 }  // namespace

@@ -149,9 +149,8 @@ class TrainPlan:
     """A validated launch of ``g2k_train_step_f32`` bound to fixed buffers:
     the fused step's outputs (pred, h, ADE/FDE sums) and the loss gradient
     [P + 2] from ONE scene-kernel launch (the producers turn each prediction
-    tile's error into the gradient; nothing is recomputed), the per-workgroup
-    gradient rows summed in a fixed order and optionally the update by the
-    same launch's last workgroups (ABI 6)."""
+    tile's error into the gradient; nothing is recomputed), the per-scene
+    gradient rows summed in a fixed order, and optionally the update."""
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *, n_frames=None,
                  ped_mask=None, stride=1, lam=LAMBDA, out=None, grad=None, stream=None,
@@ -213,7 +212,7 @@ class TrainStep:
     parameters and optimizer state.  The RMSProp mean squares start at one,
     as TF's RMSPropOptimizer initialises its "rms" slot."""
 
-    kernel_names = "g2k_scene_kernel<GRAD> (rows summed and the update run in the same launch)"
+    kernel_names = "g2k_scene_kernel<GRAD> + g2k_grad_rows_kernel<update> (one rank)"
 
     def __init__(self, params: G2KParams, pos, vislet, G, targets, n_active, h, *,
                  lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,
