@@ -57,8 +57,8 @@ REPS = [
     ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk",
      "namespace g2k {\n" + DEF + "namespace {\n\nconstexpr int kSceneChunk"),
     ("  s.total = o;\n  return s;", "  s.total = o + 4;\n  return s;"),
-    ("  if (c.tid < 8) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
-     ENTRY + "  if (c.tid < 8) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
+    ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
+     ENTRY + "  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
     ("  // the first frames' attention weights (E -> A -> As into the ring, the",
      "  G2K_TL(5, c.wv == 0);\n  // the first frames' attention weights (E -> A -> As into the ring, the"),
     ("      float4 b0, b1;\n      int f0 = read_as(",
@@ -71,11 +71,8 @@ REPS = [
     ("  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA outlives the workgroup\n}",
      "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA outlives the workgroup\n"
      "  G2K_TL(32 + c.wv, true);\n}"),
-    ("    const int hc = (!GRAD && c.X == 1) ? 2 : 1;",
-     "    G2K_TL(48, pw == 0 && fb == 0);\n    int g2k_hk = 0;\n    const int hc = (!GRAD && c.X == 1) ? 2 : 1;"),
-    ("        __builtin_amdgcn_s_setprio(0);\n        continue;\n      }",
-     "        __builtin_amdgcn_s_setprio(0);\n        G2K_TL(49 + (g2k_hk < 6 ? g2k_hk : 6), pw == 0 && fb == 0);\n"
-     "        ++g2k_hk;\n        continue;\n      }"),
+    ("    for (int i = pw; i < nh; i += NP) {",
+     "    G2K_TL(48, pw == 0 && fb == 0);\n    int g2k_hk = 0;\n    for (int i = pw; i < nh; i += NP) {"),
     ("        if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      }\n      __builtin_amdgcn_s_setprio(0);\n    }",
      "        if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      }\n      __builtin_amdgcn_s_setprio(0);\n"
      "      G2K_TL(49 + (g2k_hk < 6 ? g2k_hk : 6), pw == 0 && fb == 0);\n      ++g2k_hk;\n    }"),
