@@ -1390,7 +1390,12 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       const int f = fb + fl;
       const bool mine = !all_heads || c.X == 1 || f % c.X == c.x;
       if (fl < nrh && !mine) continue;                   // (neither As nor M wanted here)
-      if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(1);   // the first round's heads
+      // issue priority: the 4-producer (co-resident) geometry is producer-
+      // bound, so its producers outrank the chain (2 heads, 3 tiles; round 4,
+      // profiles/r4l_prio_ab.txt: eth_hotel_synth 13.4 -> 13.2 us per step);
+      // with 12 producers the chain is the critical path
+      if (NP == 4) __builtin_amdgcn_s_setprio(2);
+      else if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(1);   // the first round's heads
       const FrameHeadOut hd =
           frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                      c.sFlag + fl, f + 1,
@@ -1409,6 +1414,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       __builtin_amdgcn_s_setprio(0);
     }
     // phase 2 — predictions and errors (GRAD: and the gradient)
+    if (!GRAD && NP == 4) __builtin_amdgcn_s_setprio(3);
     if (GRAD) {
       grad_frames<PM, NLL>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
                            act_bits, acc, lsum, tg[0], true);
@@ -1441,6 +1447,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
         }
       }
     }
+    if (!GRAD && NP == 4) __builtin_amdgcn_s_setprio(0);
     if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
   }
   // metrics (and the loss): GRAD also the recurrence waves' rows (NP + w)

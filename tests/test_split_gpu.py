@@ -27,9 +27,11 @@ def _n_frames(S, F, seed):
     return nf
 
 
+@pytest.mark.parametrize("coresident", [False, True])
 @pytest.mark.parametrize("S,Nmax,H,F", [(6, 32, 128, 20), (5, 64, 256, 20), (3, 30, 64, 41),
                                         (4, 256, 256, 9)])
-def test_forward_split_equals_one_workgroup(gpu, S, Nmax, H, F):
+def test_forward_split_equals_one_workgroup(gpu, S, Nmax, H, F, coresident):
+    """coresident: the 8-wave geometry (G2K_STEP_CORESIDENT) split explicitly."""
     b = make_batch(S, Nmax, H, F=F, seed=11, h0_scale=1.0)
     t = b.to_device(gpu)
     params = fs.init_params(Nmax, seed=0, device=gpu)
@@ -37,7 +39,8 @@ def test_forward_split_equals_one_workgroup(gpu, S, Nmax, H, F):
     outs = {}
     for X in (1, 2, 3, 4):
         plan = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
-                           t["h0"], n_frames=nfr, want_attn=True, pred_layout="ped", split=X)
+                           t["h0"], n_frames=nfr, want_attn=True, pred_layout="ped", split=X,
+                           coresident=coresident)
         runs = []
         for _ in range(3):                     # the tickets are re-armed by every call
             o = plan.run()
