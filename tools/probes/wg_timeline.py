@@ -85,7 +85,19 @@ STAGE = [
      "  G2K_TL(58 + (c.wv < kRecW ? 0 : 1), (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"
      "  __builtin_amdgcn_s_waitcnt(0xc07f);                           // lgkmcnt(0)\n  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2"),
 ]
-REPS += STAGE
+PROLOGUE = [
+    ("    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first\n",
+     "    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first\n"
+     "    G2K_TL(60, c.wv == 0);\n"),
+    ("    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)",
+     "    G2K_TL(61, c.wv == 0);\n    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)"),
+    ("    scalars();\n    scene_recurrence<TPW, NP>(a, lay, c);",
+     "    scalars();\n    G2K_TL(62, c.wv == 0);\n    scene_recurrence<TPW, NP>(a, lay, c);"),
+    ("  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)\n",
+     "  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)\n"
+     "  G2K_TL(63, (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"),
+]
+REPS += STAGE + PROLOGUE
 FINE = {48: "heads loop entry", 49: "head 1", 50: "head 2", 51: "head 3", 52: "head 4", 53: "head 5", 54: "head 6", 55: "head 7+"}
 
 
@@ -217,6 +229,9 @@ def run(config, nstreams, split=0, cores=False):
     st = {"B1 rec0": rel(56) - start, "B1 prod0": rel(57) - start, "staged rec0": rel(58) - start,
           "staged prod0": rel(59) - start, "B2 rec0": rel(5) - start, "chain0": rel(6) - start}
     print("lead (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in st.items()))
+    pro = {"pos dma issued": rel(60) - start, "segments issued": rel(61) - start,
+           "rec0 scalars": rel(62) - start, "loads landed (w0 or p0)": rel(63) - start}
+    print("prologue (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in pro.items()))
     # co-residency: workgroups sharing a CU (XCC_ID, HW_ID[15:8]) at the same time
     cu = (r[:, 3] << 8) | ((r[:, 2] >> 8) & 0xff)
     over = np.zeros(n, dtype=int)
