@@ -97,7 +97,17 @@ PROLOGUE = [
      "  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)\n"
      "  G2K_TL(63, (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"),
 ]
-REPS += STAGE + PROLOGUE
+TRAIN = [
+    ("      // every worker done with the chunk's frames -> its dU rows into dV\n",
+     "      G2K_TL(44, pw == 0 && fb == 0);\n      // every worker done with the chunk's frames -> its dU rows into dV\n"),
+    ("      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)",
+     "      G2K_TL(45, pw == 0 && fb == 0);\n      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)"),
+    ("  grad_priv_sum(c, NP);                                // then all producers see sGAcc",
+     "  G2K_TL(46, pw == 0);\n  grad_priv_sum(c, NP);                                // then all producers see sGAcc"),
+    ("  // the small blocks and dWo, entry by entry over all producer lanes",
+     "  G2K_TL(47, pw == 0);\n  // the small blocks and dWo, entry by entry over all producer lanes"),
+]
+REPS += STAGE + PROLOGUE + TRAIN
 FINE = {48: "heads loop entry", 49: "head 1", 50: "head 2", 51: "head 3", 52: "head 4", 53: "head 5", 54: "head 6", 55: "head 7+"}
 
 
@@ -154,10 +164,17 @@ def run(config, nstreams, split=0, cores=False):
     plans = []
     for k in range(K):
         t = {key: (v.clone() if isinstance(v, torch.Tensor) else v) for key, v in base.items()}
-        plans.append(fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
-                                 t["h0"], n_frames=t["n_frames"], ped_mask=t["ped_mask"],
-                                 stride=b.stride, stream=streams[k % nstreams], pred_layout="ped",
-                                 split=split, coresident=cores))
+        if os.environ.get("TL_TRAIN"):                  # train mode: the gradient launch
+            from multimodaltraj_2_amd import train_step as ts
+            plans.append(ts.TrainPlan(params, t["pos"], t["vislet"], t["G"], t["targets"],
+                                      t["n_active"], t["h0"], n_frames=t["n_frames"],
+                                      ped_mask=t["ped_mask"], stride=b.stride,
+                                      stream=streams[k % nstreams], pred_layout="ped", split=split))
+        else:
+            plans.append(fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
+                                     t["h0"], n_frames=t["n_frames"], ped_mask=t["ped_mask"],
+                                     stride=b.stride, stream=streams[k % nstreams], pred_layout="ped",
+                                     split=split, coresident=cores))
     tags = {int(p.out.h.data_ptr() >> 8) & 0xffffffff: k for k, p in enumerate(plans)}
     for _ in range(3):
         for p in plans:
@@ -191,6 +208,8 @@ def run(config, nstreams, split=0, cores=False):
         t0[xcc == x] = r[xcc == x, 4].min()
     rel = lambda col: (r[:, col] - t0) % (1 << 32)   # noqa: E731
     np_ = 4 if fs.step_coresidency(S, 20, H, Nmax, b.pos.shape[1], b.stride, cores) == 2 else 12
+    if os.environ.get("TL_TRAIN"):
+        np_ = 8
     start, ex = rel(4), np.max([rel(32 + w) for w in range(4 + np_)], axis=0)
     span_cyc = np.median([ex[xcc == x].max() for x in np.unique(xcc)])
     ghz = span_cyc / wall_us / 1e3
@@ -231,6 +250,11 @@ def run(config, nstreams, split=0, cores=False):
     print("lead (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in st.items()))
     pro = {"pos dma issued": rel(60) - start, "segments issued": rel(61) - start,
            "rec0 scalars": rel(62) - start, "loads landed (w0 or p0)": rel(63) - start}
+    if os.environ.get("TL_TRAIN"):
+        tr = {"heads done": rel(8) - start, "grad frames done": rel(44) - start, "chunk synced": rel(45) - start,
+              "tickets (all metrics)": rel(46) - start, "dWi done": rel(47) - start,
+              "prod0 end": rel(20) - start, "chain end": rel(7) - start, "exit": ex - start}
+        print("train, producer 0 (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in tr.items()))
     print("prologue (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in pro.items()))
     # co-residency: workgroups sharing a CU (XCC_ID, HW_ID[15:8]) at the same time
     cu = (r[:, 3] << 8) | ((r[:, 2] >> 8) & 0xff)
