@@ -606,10 +606,23 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     scene_rm(lay, c, rm);
     const int fl = c.wv;
     const bool mine = c.X == 1 || fl % c.X == 0;
-    frame_head(c.sm, c.sV, c.sVG, fl * a.d.stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
-               c.sFlag + fl, fl + 1,
-               a.A_out && mine ? a.A_out + ((size_t)c.s * a.d.F + fl) * kD * kD : nullptr, nullptr,
-               nullptr, c.L, c.q, /*want_m=*/false);
+    // the 4-producer geometry: these frames' M too (the producers skip them)
+    constexpr bool kRecM = NP == 4;
+    const FrameHeadOut hd =
+        frame_head(c.sm, c.sV, c.sVG, fl * a.d.stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
+                   c.sFlag + fl, fl + 1,
+                   a.A_out && mine ? a.A_out + ((size_t)c.s * a.d.F + fl) * kD * kD : nullptr,
+                   kRecM && a.cost_out && mine ? a.cost_out + ((size_t)c.s * a.d.F + fl) * kT * kT : nullptr,
+                   nullptr, c.L, c.q, /*want_m=*/kRecM && mine);
+    if (kRecM && mine) {
+      if (c.L < kL && c.q < 2) {
+        float* m = c.sMring + fl * kL2 * kT;
+        *reinterpret_cast<float4*>(m + c.L * kT + 4 * c.q) = make_float4(hd.mT0[0], hd.mT0[1], hd.mT0[2], hd.mT0[3]);
+        *reinterpret_cast<float4*>(m + (kL + c.L) * kT + 4 * c.q) = make_float4(hd.mT1[0], hd.mT1[1], hd.mT1[2], hd.mT1[3]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (c.lane == 0) lds_store_flag(c.sMflag + fl, fl + 1);
+    }
     __builtin_amdgcn_s_setprio(0);
   }
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
@@ -1389,7 +1402,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       const int fl = hb + hs * i;
       const int f = fb + fl;
       const bool mine = !all_heads || c.X == 1 || f % c.X == c.x;
-      if (fl < nrh && !mine) continue;                   // (neither As nor M wanted here)
+      if (fl < nrh && (!mine || (NP == 4 && !GRAD))) continue;   // (a recurrence wave formed As, and M)
       // issue priority: the 4-producer (co-resident) geometry is producer-
       // bound, so its producers outrank the chain (2 heads, 3 tiles; round 4,
       // profiles/r4l_prio_ab.txt: eth_hotel_synth 13.4 -> 13.2 us per step);
