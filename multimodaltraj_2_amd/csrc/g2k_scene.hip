@@ -521,10 +521,15 @@ __device__ __forceinline__ void scene_rm(const SceneLayout& lay, const SceneCtx&
 }
 
 // Frames 0 .. n-1 whose As the recurrence waves form themselves (one frame
-// per wave, right after the first staging; the scene's recurrence workgroup)
+// per wave — two in the 4-producer geometry when a frame has 3 or more
+// prediction tiles, round 4: kfold4 10.8 -> 10.6 us per step, relational
+// 18.7 -> 18.4, the 2-tile shapes neutral — right after the first staging;
+// the scene's recurrence workgroup)
+template <int NP>
 __device__ __forceinline__ int rec_head_frames(const SceneLayout& lay, const SceneCtx& c) {
   const int n = c.nf < lay.fc ? c.nf : lay.fc;
-  return n < kRecW ? n : kRecW;
+  const int m = kRecW * (NP == 4 && c.ntact >= 3 ? 2 : 1);
+  return n < m ? n : m;
 }
 
 // Chunk staging shared by both roles (every wave takes part).  The chunk's
@@ -600,11 +605,10 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   // priority: the producers reach their first heads only after their loop
   // set-up (thousands of cycles of scalar work on the CU's one scalar unit);
   // they form only M for these frames
-  if (live && c.wv < rec_head_frames(lay, c)) {
+  for (int fl = c.wv; live && fl < rec_head_frames<NP>(lay, c); fl += kRecW) {
     __builtin_amdgcn_s_setprio(3);
     float rm[4];
     scene_rm(lay, c, rm);
-    const int fl = c.wv;
     const bool mine = c.X == 1 || fl % c.X == 0;
     // the 4-producer geometry: these frames' M too (the producers skip them)
     constexpr bool kRecM = NP == 4;
@@ -1397,7 +1401,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // of the first chunk's frames 0 .. nrh - 1 themselves (M only here).
     const bool all_heads = a.h_in != nullptr && c.x == 0;
     const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : c.X, nh = all_heads ? cnt : own.n;
-    const int nrh = all_heads && fb == 0 ? rec_head_frames(lay, c) : 0;
+    const int nrh = all_heads && fb == 0 ? rec_head_frames<NP>(lay, c) : 0;
     for (int i = pw; i < nh; i += NP) {
       const int fl = hb + hs * i;
       const int f = fb + fl;
