@@ -83,6 +83,7 @@ STAGE = [
      "  G2K_TL(56 + (c.wv < kRecW ? 0 : 1), (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"),
     ("  __builtin_amdgcn_s_waitcnt(0xc07f);                           // lgkmcnt(0)\n  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2",
      "  G2K_TL(58 + (c.wv < kRecW ? 0 : 1), (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"
+     "  G2K_TL(24 + (c.wv - kRecW) % 8, c.wv >= kRecW && c.wv < kRecW + 4 && fb == 0);\n"
      "  __builtin_amdgcn_s_waitcnt(0xc07f);                           // lgkmcnt(0)\n  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2"),
 ]
 PROLOGUE = [
@@ -247,6 +248,8 @@ def run(config, nstreams, split=0, cores=False):
     print("producer 0:", "  ".join(fine))
     st = {"B1 rec0": rel(56) - start, "B1 prod0": rel(57) - start, "staged rec0": rel(58) - start,
           "staged prod0": rel(59) - start, "B2 rec0": rel(5) - start, "chain0": rel(6) - start}
+    if np_ == 4:
+        print("staging task done per producer (medians):", "  ".join(f"p{p} {np.median(rel(24 + p) - start):.0f}" for p in range(4)))
     print("lead (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in st.items()))
     pro = {"pos dma issued": rel(60) - start, "segments issued": rel(61) - start,
            "rec0 scalars": rel(62) - start, "loads landed (w0 or p0)": rel(63) - start}
