@@ -1494,12 +1494,11 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   for (int t = pw; t < ntile_all; t += NP) {
     const int n0 = 16 * t, n = n0 + L;
     f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
-    if (n0 < c.nact) {
-      // one chunk: the whole window is still in LDS (sPos, pitch lay.pp);
-      // else the position rows again from global memory
-      const bool in_lds = lay.fc >= F;
-      const float* prow = in_lds ? c.sPos : a.pos + (size_t)c.s * a.d.W * Nmax * 2;
-      const int pitch = in_lds ? lay.pp : 2 * Nmax;
+    // one chunk: the whole window is still in LDS (sPos, pitch lay.pp);
+    // else the position rows again from global memory.  Two inlined copies,
+    // so the LDS one reads by ds_read (one generic pointer for both made
+    // them flat loads, counted on vmcnt behind the row's stores)
+    auto dwi = [&](const float* prow, int pitch) {
       const int nks = (lay.wtot + 3) / 4;
       const int nc = n < c.nact ? n : 0;
       // four k-steps' position loads in flight (clamped rows, selected after)
@@ -1520,6 +1519,10 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
           acc4 = mfma4(av, bv, acc4);
         }
       }
+    };
+    if (n0 < c.nact) {
+      if (lay.fc >= F) dwi(c.sPos, lay.pp);
+      else dwi(a.pos + (size_t)c.s * a.d.W * Nmax * 2, 2 * Nmax);
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -1644,10 +1647,6 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   c.sNllA = smem + lay.o_nlla; c.sNllW = smem + lay.o_nllw;
   c.sNllR = smem + lay.o_nllr; c.sNllC = smem + lay.o_nllc;
   if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;  // sequence words, ticket
-  if (GRAD) {                                          // accumulators and their sequence words
-    for (int i = c.tid; i < lay.o_gseq + rup4(2 + c.ntiles) - lay.o_gacc; i += NT) smem[lay.o_gacc + i] = 0.f;
-    if (a.grad_ticket && blockIdx.x == 0 && c.tid == 0) *a.grad_ticket = 0;   // this step's update ticket
-  }
   if (F > 0) {
     // issued before n_active / n_frames arrive: the first chunk's window for
     // min(F, fc) frames (a scene with fewer frames reads rows it ignores)
@@ -1695,6 +1694,17 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
       c.sMflag[c.tid] = 0;
     }
   }
+  // GRAD: the gradient accumulators and their sequence words zeroed (16 B
+  // per lane; the region is 16-B aligned and a multiple of 4 floats) after
+  // the prologue's loads are in flight, under their latency (zeroed ahead of
+  // the LDS-DMA issue they put it ~4.5k cycles later than a forward launch's)
+  auto zero_grad = [&] {
+    if (!GRAD) return;
+    const int n4 = (lay.o_gseq + rup4(2 + c.ntiles) - lay.o_gacc) >> 2;
+    float4* z = reinterpret_cast<float4*>(smem + lay.o_gacc);
+    for (int i = c.tid; i < n4; i += NT) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.grad_ticket && blockIdx.x == 0 && c.tid == 0) *a.grad_ticket = 0;   // this step's update ticket
+  };
   // scene scalars: one scalar round trip (the recurrence's h and the
   // producers' ped_mask word are loaded later, off the prologue's burst)
   auto scalars = [&] {
@@ -1703,6 +1713,7 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
     c.nact = clampi(na, 0, Nmax);
     c.nf = a.n_frames ? clampi(nf, 0, F) : F;
     c.ntact = (c.nact + 15) >> 4;                      // tiles holding active pedestrians
+    zero_grad();
     if (c.nf == 0) __syncthreads();   // no staging barrier will publish the initialised words
   };
   if (c.wv < kRecW) {

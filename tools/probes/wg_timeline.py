@@ -20,14 +20,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "ab", "libg2k_timeline.so")
-NREC = 64
+NREC = 80
 
 DEF = r"""
-__device__ unsigned g2k_tl_buf[8192 * 64];
+__device__ unsigned g2k_tl_buf[8192 * 80];
 __device__ unsigned g2k_tl_ctr;
 #define G2K_TL(k, cond) do { if ((cond) && c.lane == 0) { \
   const int _s = *reinterpret_cast<const int*>(c.sWi - lay.o_wi + lay.total); \
-  g2k_tl_buf[(size_t)_s * 64 + (k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
+  g2k_tl_buf[(size_t)_s * 80 + (k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
 """
 EXPORT = r"""
 extern "C" int g2k_tl_copy(unsigned* host, int n) {
@@ -45,7 +45,7 @@ ENTRY = r"""  if (c.tid == 0) {
     const unsigned t0 = (unsigned)__builtin_amdgcn_s_memtime();
     const int s_ = (int)(atomicAdd(&g2k_tl_ctr, 1u) & 8191u);   // (wraps: warm-up launches)
     reinterpret_cast<int*>(smem + lay.total)[0] = s_;
-    unsigned* r = g2k_tl_buf + (size_t)s_ * 64;
+    unsigned* r = g2k_tl_buf + (size_t)s_ * 80;
     r[0] = blockIdx.x + 1;
     r[1] = (unsigned)((uintptr_t)a.h_out >> 8);
     r[2] = __builtin_amdgcn_s_getreg(63492);
@@ -107,6 +107,16 @@ TRAIN = [
      "  G2K_TL(46, pw == 0);\n  grad_priv_sum(c, NP);                                // then all producers see sGAcc"),
     ("  // the small blocks and dWo, entry by entry over all producer lanes",
      "  G2K_TL(47, pw == 0);\n  // the small blocks and dWo, entry by entry over all producer lanes"),
+]
+TRAIN += [
+    ("      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)\n",
+     "      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)\n"
+     "      G2K_TL(64, pw == 0 && fb == 0);\n"),
+    ("  poll_word(c.sTicket, NP + kRecW);\n", "  G2K_TL(65, pw == 0);\n  poll_word(c.sTicket, NP + kRecW);\n"),
+    ("  poll_word(c.sGseq + 1, NP);\n", "  poll_word(c.sGseq + 1, NP);\n  G2K_TL(66, pw == 0);\n"),
+    ("      if (c.lane == 0) atomicAdd(c.sGseq, 1);\n    }\n  }\n  if (NLL) nll_worker_reduce(c, NP + c.wv);",
+     "      G2K_TL(67, c.wv == 0);\n      if (c.lane == 0) atomicAdd(c.sGseq, 1);\n    }\n  }\n"
+     "  if (NLL) nll_worker_reduce(c, NP + c.wv);"),
 ]
 REPS += STAGE + PROLOGUE + TRAIN
 FINE = {48: "heads loop entry", 49: "head 1", 50: "head 2", 51: "head 3", 52: "head 4", 53: "head 5", 54: "head 6", 55: "head 7+"}
@@ -256,9 +266,17 @@ def run(config, nstreams, split=0, cores=False):
     if os.environ.get("TL_TRAIN"):
         tr = {"heads done": rel(8) - start, "grad frames done": rel(44) - start, "chunk synced": rel(45) - start,
               "tickets (all metrics)": rel(46) - start, "dWi done": rel(47) - start,
-              "prod0 end": rel(20) - start, "chain end": rel(7) - start, "exit": ex - start}
+              "prod0 end": rel(20) - start, "chain end": rel(7) - start, "exit": ex - start,
+              "flushed": rel(64) - start, "metrics published": rel(65) - start,
+              "priv summed": rel(66) - start, "rec0 grad frame done": rel(67) - start}
         print("train, producer 0 (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in tr.items()))
     print("prologue (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in pro.items()))
+    # per XCD: medians / maxima of B1, B2 and the exit (the launch ends with its slowest workgroup)
+    b1 = rel(56) - start
+    print("per XCD (B1 med/max, B2 med/max, exit med/max):", "  ".join(
+        f"x{int(x)} {np.median(b1[xcc == x]):.0f}/{b1[xcc == x].max():.0f} "
+        f"{np.median((rel(5) - start)[xcc == x]):.0f}/{(rel(5) - start)[xcc == x].max():.0f} "
+        f"{np.median((ex - start)[xcc == x]):.0f}/{(ex - start)[xcc == x].max():.0f}" for x in np.unique(xcc)))
     # co-residency: workgroups sharing a CU (XCC_ID, HW_ID[15:8]) at the same time
     cu = (r[:, 3] << 8) | ((r[:, 2] >> 8) & 0xff)
     over = np.zeros(n, dtype=int)
