@@ -1,9 +1,10 @@
 """Where the fixed cost of a short timed region goes (development probe, not
 product code): bench.py's default line at --steps K with the timed graph
-(a) as bench.py does it (hipGraphUpload at capture), (b) without the upload
-(G2K_BENCH_NO_UPLOAD=1, set by the caller), (c) `prereplay`: the timed graph
+(a) `default`: as bench.py does it, (b) `prereplay`: the timed graph
 replayed once untimed first (diagnosis only — extra warm-up steps, not a
-bench.py mode).
+bench.py mode).  A hipGraphUpload of the timed graph at capture (through a
+second handle on the HIP runtime) measured no different from (a) and was
+dropped.
     python tools/probes/graph_overhead.py MODE K
 """
 import os
