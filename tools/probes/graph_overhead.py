@@ -2,9 +2,10 @@
 product code): bench.py's default line at --steps K with the timed graph
 (a) `default`: as bench.py does it, (b) `prereplay`: the timed graph
 replayed once untimed first (diagnosis only — extra warm-up steps, not a
-bench.py mode).  A hipGraphUpload of the timed graph at capture (through a
-second handle on the HIP runtime) measured no different from (a) and was
-dropped.
+bench.py mode), (c) `upload`: hipGraphUpload of every captured graph on the
+stream its replays run on, through torch's own HIP runtime (soname
+libamdhip64.so.7; r5e/r5f loaded a second copy of the runtime by the
+unversioned name, which measured nothing).
     python tools/probes/graph_overhead.py MODE K
 """
 import os
@@ -28,8 +29,27 @@ def timed_graph_prereplay(step, n, warmup, dist, sync, stream, side=()):
     return time.perf_counter() - t0, gm
 
 
+def patch_upload():
+    import ctypes
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so.7")          # torch's runtime (already loaded)
+    hip.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    hip.hipGraphUpload.restype = ctypes.c_int
+    init = bench.GraphSteps.__init__
+
+    def init_upload(self, *a, **k):
+        init(self, *a, **k)
+        rc = hip.hipGraphUpload(ctypes.c_void_p(self.g.raw_cuda_graph_exec()),
+                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+    bench.GraphSteps.__init__ = init_upload
+
+
 if __name__ == "__main__":
     mode, k = sys.argv[1], sys.argv[2]
     if mode == "prereplay":
         bench.timed_graph = timed_graph_prereplay
+    if mode == "upload":
+        patch_upload()
     sys.exit(bench.main(["--no-cpu-baseline", "--no-train", "--steps", k]))
