@@ -5,7 +5,9 @@ replayed once untimed first (diagnosis only — extra warm-up steps, not a
 bench.py mode), (c) `upload`: hipGraphUpload of every captured graph on the
 stream its replays run on, through torch's own HIP runtime (soname
 libamdhip64.so.7; r5e/r5f loaded a second copy of the runtime by the
-unversioned name, which measured nothing).
+unversioned name, which measured nothing), (d) `onstream`: every replay
+launched with the capture stream current (bench.py replays on the default
+stream).
     python tools/probes/graph_overhead.py MODE K
 """
 import os
@@ -46,10 +48,27 @@ def patch_upload():
     bench.GraphSteps.__init__ = init_upload
 
 
+def patch_onstream():
+    import torch
+    init = bench.GraphSteps.__init__
+
+    def init_keep(self, step, n, stream, *a, **k):
+        init(self, step, n, stream, *a, **k)
+        self._stream = stream
+
+    def replay(self):
+        with torch.cuda.stream(self._stream):
+            self.g.replay()
+    bench.GraphSteps.__init__ = init_keep
+    bench.GraphSteps.replay = replay
+
+
 if __name__ == "__main__":
     mode, k = sys.argv[1], sys.argv[2]
     if mode == "prereplay":
         bench.timed_graph = timed_graph_prereplay
     if mode == "upload":
         patch_upload()
+    if mode == "onstream":
+        patch_onstream()
     sys.exit(bench.main(["--no-cpu-baseline", "--no-train", "--steps", k]))
