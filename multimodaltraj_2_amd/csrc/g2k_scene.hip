@@ -1143,6 +1143,11 @@ __device__ __forceinline__ unsigned scene_act_bits(const SceneCtx& c, uint32_t w
 // recurrence waves (one each, after their recurrence), so the producers'
 // share shrinks when they have at least two frames each.
 __device__ __forceinline__ int grad_rec_frames(int cnt, int NP) { return cnt >= 2 * NP ? kRecW : 0; }
+// ... split by tile when a frame has two or more: the recurrence wave takes
+// tiles [0, h) (it starts at the chain's end), producer w (w < R, free after
+// its own frames) tiles [h, ntact) of the same frame; each adds its partial
+// dM's weight-side terms (frame_grad is linear in dM) into its own sums
+__device__ __forceinline__ int grad_rec_tiles(int ntact) { return ntact >= 2 ? (ntact + 1) / 2 : ntact; }
 
 // The targets of tile t of chunk frame fl in pred_tile's order (pedestrian
 // 16 t + L, floats 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row, zero
@@ -1198,11 +1203,13 @@ template <bool PM, bool NLL>
 __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int slot, int fb, int f0, int fstep,
                                             int fend, unsigned act_bits, float (&acc)[5],
-                                            float& lsum, float2 (&tg)[4], bool preloaded) {
-  const int Nmax = a.d.Nmax, F = a.d.F, L = c.L, q = c.q, ntact = c.ntact;
+                                            float& lsum, float2 (&tg)[4], bool preloaded,
+                                            int t0 = 0, int t1 = -1) {
+  const int Nmax = a.d.Nmax, F = a.d.F, L = c.L, q = c.q;
+  const int ntact = t1 < 0 ? c.ntact : t1;             // tiles [t0, ntact) of each frame
   const brsrc tgr = scene_targets_rsrc(a, c.s);
   if (!preloaded) {
-    load_targets(tgr, Nmax, c.nact, fb, f0, 0, f0 < fend, L, q, tg, lay.tfb);
+    load_targets(tgr, Nmax, c.nact, fb, f0, t0, f0 < fend, L, q, tg, lay.tfb);
     balance_stores<PM>(a);
   }
   float* ys = c.sY + slot * kL2 * kYP;
@@ -1213,9 +1220,9 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
     poll_flag(c.sMflag + fl, f + 1);                     // M of this frame (a producer's head)
     const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)c.s * F + f) * kL2 * Nmax : a.targets,
                                 a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
-    for (int t = 0; t < ntact; ++t) {
+    for (int t = t0; t < ntact; ++t) {
       const bool nxt = t + 1 < ntact;                    // the next tile: this frame's, else the next frame's
-      const int nfl = nxt ? fl : fl + fstep, nt = nxt ? t + 1 : 0;
+      const int nfl = nxt ? fl : fl + fstep, nt = nxt ? t + 1 : t0;
       f32x4 dWoT;
       pred_tile<true, PM, NLL>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u,
                                Nmax, c.nact, t, L, q, acc, lsum, dm, dWoT,
@@ -1435,6 +1442,11 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     if (GRAD) {
       grad_frames<PM, NLL>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
                            act_bits, acc, lsum, tg[0], true);
+      if (pw < R && grad_rec_tiles(ntact) < ntact) {    // the recurrence waves' frames' other tiles
+        const int fl = own.fo + c.X * (gend + pw);
+        grad_frames<PM, NLL>(a, lay, c, pw, fb, fl, 1, fl + 1, act_bits, acc, lsum, tg[0], false,
+                             grad_rec_tiles(ntact), ntact);
+      }
       // every worker done with the chunk's frames -> its dU rows into dV
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) atomicAdd(c.sGseq, 1);
@@ -1595,7 +1607,7 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
       grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, own.fo + c.X * (own.n - R + c.wv), c.X * R,
                            own.fo + c.X * own.n,
                            scene_act_bits(c, scene_mask_word(a, lay, c)),
-                           acc, lsum, tg, false);
+                           acc, lsum, tg, false, 0, grad_rec_tiles(c.ntact));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (c.lane == 0) atomicAdd(c.sGseq, 1);
     }
