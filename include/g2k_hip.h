@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define G2K_ABI_VERSION 6
+#define G2K_ABI_VERSION 7
 
 enum {
   G2K_OK = 0,
@@ -90,10 +90,14 @@ typedef struct g2k_dims {
  * than the device has CUs spreads each scene's frames over x workgroups, the
  * first of which also runs the recurrence; g2k_step_split reports x).  x > 1
  * needs the workspace (g2k_step_workspace_bytes / g2k_train_workspace_bytes /
- * g2k_grad_workspace_bytes) zero-filled before its first use, in stream order
- * with the first launch (g2k_workspace_init: a memset on the launch stream);
- * every call leaves it zero-filled again.  One workspace per stream: two
- * launches in flight must not share one. */
+ * g2k_grad_workspace_bytes); its contents need no initialisation: every launch
+ * zeroes the scene tickets in it on its own stream first (a memset ahead of
+ * the kernel), so no earlier call — an aborted one included — can leave state
+ * behind.  One workspace per stream: two launches in flight must not share
+ * one.  The automatic choice and the workspace sizes depend on the CU count of
+ * the device current when they are queried (hipGetDevice: these planning
+ * calls initialise the HIP runtime); a launch re-derives them for the device
+ * current at launch time and rejects a workspace smaller than that needs. */
 #define G2K_STEP_SPLIT_SHIFT 8
 #define G2K_STEP_SPLIT_MASK (7 << G2K_STEP_SPLIT_SHIFT)
 #define G2K_STEP_SPLIT(x) ((x) << G2K_STEP_SPLIT_SHIFT)
@@ -123,8 +127,9 @@ int64_t g2k_step_workspace_bytes(const g2k_dims* d);
 /* Workgroups per scene the step / train entry points use for `d` (the
  * G2K_STEP_SPLIT request, or the automatic choice); -1 on invalid dims. */
 int32_t g2k_step_split(const g2k_dims* d);
-/* Zero-fill `workspace_bytes` bytes of a workspace on `stream` (hipMemsetAsync):
- * the stream-ordered first fill the split tickets need. */
+/* Zero-fill `workspace_bytes` bytes of a workspace on `stream` (hipMemsetAsync).
+ * (ABI 6 and earlier required it before a split workspace's first use; since
+ * ABI 7 every launch zeroes its tickets itself and this is optional.) */
 int g2k_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
 
 /*

@@ -92,7 +92,7 @@ SYMBOLS = {
                                      c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class G2KLibraryError(RuntimeError):

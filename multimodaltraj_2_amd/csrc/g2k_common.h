@@ -407,7 +407,7 @@ struct StepArgs {
   float* grad_rows;   // [S * X][P + 2] or NULL (X = scene_split: one row per workgroup)
   int* grad_ticket;   // train step with update: zeroed by workgroup 0 for the gradient-row
                       // sum's last-workgroup count (g2k_train.hip), or NULL
-  int* scene_ticket;  // X > 1: [S] workgroups of a scene done (zero between launches)
+  int* scene_ticket;  // X > 1: [S] workgroups of a scene done (zeroed on the stream before each launch)
   float* met_part;    // X > 1: [S][X][8] the workgroups' metric partials
 };
 

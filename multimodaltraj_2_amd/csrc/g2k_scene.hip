@@ -521,14 +521,14 @@ __device__ __forceinline__ void scene_rm(const SceneLayout& lay, const SceneCtx&
 }
 
 // Frames 0 .. n-1 whose As the recurrence waves form themselves (one frame
-// per wave — two in the 4-producer geometry when a frame has 3 or more
+// per wave — two in the co-resident geometry (CR) when a frame has 3 or more
 // prediction tiles, round 4: kfold4 10.8 -> 10.6 us per step, relational
 // 18.7 -> 18.4, the 2-tile shapes neutral — right after the first staging;
 // the scene's recurrence workgroup)
-template <int NP>
+template <bool CR>
 __device__ __forceinline__ int rec_head_frames(const SceneLayout& lay, const SceneCtx& c) {
   const int n = c.nf < lay.fc ? c.nf : lay.fc;
-  const int m = kRecW * (NP == 4 && c.ntact >= 3 ? 2 : 1);
+  const int m = kRecW * (CR && c.ntact >= 3 ? 2 : 1);
   return n < m ? n : m;
 }
 
@@ -574,7 +574,7 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
 // HBM burst, which every wave's B1 waits for, stays free of it) and its
 // softmax numerators are formed there too; after B2 the waves form As of the
 // first frames themselves and start the chain.
-template <int TPW, int NP>
+template <int TPW, int NP, bool CR>
 __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneLayout& lay,
                                                  const SceneCtx& c) {
   constexpr int NT = 64 * (kRecW + NP);
@@ -605,13 +605,16 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   // priority: the producers reach their first heads only after their loop
   // set-up (thousands of cycles of scalar work on the CU's one scalar unit);
   // they form only M for these frames
-  for (int fl = c.wv; live && fl < rec_head_frames<NP>(lay, c); fl += kRecW) {
+  for (int fl = c.wv; live && fl < rec_head_frames<CR>(lay, c); fl += kRecW) {
     __builtin_amdgcn_s_setprio(3);
     float rm[4];
     scene_rm(lay, c, rm);
     const bool mine = c.X == 1 || fl % c.X == 0;
-    // the 4-producer geometry: these frames' M too (the producers skip them)
-    constexpr bool kRecM = NP == 4;
+    // the co-resident geometry: these frames' M too (its producers skip
+    // them).  Not in train mode: there the producers form these frames' M
+    // AND the cost their gradient terms read (sCost), and the M flag must not
+    // be published before that cost is in LDS
+    constexpr bool kRecM = CR;
     const FrameHeadOut hd =
         frame_head(c.sm, c.sV, c.sVG, fl * a.d.stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                    c.sFlag + fl, fl + 1,
@@ -1311,8 +1314,10 @@ __device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCt
     // split scene: this workgroup's row into the scene's partials (stores that
     // write through to the coherence point, completed before the ticket); the
     // workgroup drawing the scene's last ticket sums the rows in workgroup
-    // order (deterministic) after an acquire fence, writes the metrics row and
-    // re-arms the ticket for the next launch
+    // order (deterministic) after an acquire fence and writes the metrics row.
+    // The tickets are zeroed in stream order before every launch
+    // (scene_step_launch), so a stale or partial earlier launch cannot leave
+    // one off
     const int X = c.X, x = c.x;
     float* part = a.met_part + (size_t)c.s * X * 8;
     if (lane < 8) __hip_atomic_store(part + x * 8 + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1327,13 +1332,12 @@ __device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCt
       for (int p = 0; p < X; ++p)
         v += __hip_atomic_load(part + p * 8 + l8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (lane == 0) __hip_atomic_store(a.scene_ticket + c.s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (lane < 8) store_wt(a.metrics + (size_t)c.s * 8 + lane, v);
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
-template <int NP, bool GRAD, bool PM, bool NLL>
+template <int NP, bool GRAD, bool PM, bool NLL, bool CR>
 __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLayout& lay,
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
@@ -1408,17 +1412,17 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // of the first chunk's frames 0 .. nrh - 1 themselves (M only here).
     const bool all_heads = a.h_in != nullptr && c.x == 0;
     const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : c.X, nh = all_heads ? cnt : own.n;
-    const int nrh = all_heads && fb == 0 ? rec_head_frames<NP>(lay, c) : 0;
+    const int nrh = all_heads && fb == 0 ? rec_head_frames<CR>(lay, c) : 0;
     for (int i = pw; i < nh; i += NP) {
       const int fl = hb + hs * i;
       const int f = fb + fl;
       const bool mine = !all_heads || c.X == 1 || f % c.X == c.x;
-      if (fl < nrh && (!mine || (NP == 4 && !GRAD))) continue;   // (a recurrence wave formed As, and M)
-      // issue priority: the 4-producer (co-resident) geometry is producer-
-      // bound, so its producers outrank the chain (2 heads, 3 tiles; round 4,
+      if (fl < nrh && (!mine || CR)) continue;   // (a recurrence wave formed As, and M under CR)
+      // issue priority: the co-resident geometry is producer-bound, so its
+      // producers outrank the chain (2 heads, 3 tiles; round 4,
       // profiles/r4l_prio_ab.txt: eth_hotel_synth 13.4 -> 13.2 us per step);
       // with 12 producers the chain is the critical path
-      if (NP == 4) __builtin_amdgcn_s_setprio(2);
+      if (CR) __builtin_amdgcn_s_setprio(2);
       else if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(1);   // the first round's heads
       const FrameHeadOut hd =
           frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
@@ -1438,7 +1442,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       __builtin_amdgcn_s_setprio(0);
     }
     // phase 2 — predictions and errors (GRAD: and the gradient)
-    if (!GRAD && NP == 4) __builtin_amdgcn_s_setprio(3);
+    if (CR) __builtin_amdgcn_s_setprio(3);
     if (GRAD) {
       grad_frames<PM, NLL>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
                            act_bits, acc, lsum, tg[0], true);
@@ -1476,7 +1480,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
         }
       }
     }
-    if (!GRAD && NP == 4) __builtin_amdgcn_s_setprio(0);
+    if (CR) __builtin_amdgcn_s_setprio(0);
     if (fb + lay.fc < c.nf) __syncthreads();                    // B3: chunk done (not after the last)
   }
   // metrics (and the loss): GRAD also the recurrence waves' rows (NP + w)
@@ -1629,6 +1633,11 @@ __attribute__((amdgpu_waves_per_eu(scene_waves_per_eu<TPW, NP>())))
 g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   constexpr int NT = 64 * (kRecW + NP);
   constexpr int kRB = 16 * kRecW;
+  // the co-resident geometry (8 waves, two workgroups per CU, forward only):
+  // its measured scheduling rules (producer priorities, the recurrence waves'
+  // extra heads and M) apply only to it — not to the H = 512 or train-mode
+  // 4-producer builds, which run one workgroup per CU
+  constexpr bool CR = scene_waves_per_eu<TPW, NP>() > 1 && !GRAD;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   // every kernel-argument line the prologue reads, in ONE scalar-load round
   // trip (left alone, the compiler asks for the n_active / h_in line only
@@ -1730,11 +1739,11 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   };
   if (c.wv < kRecW) {
     scalars();
-    scene_recurrence<TPW, NP>(a, lay, c);
+    scene_recurrence<TPW, NP, CR>(a, lay, c);
     if (GRAD) rec_grad_work<NP, PM, NLL>(a, lay, c);
   } else {
     scalars();
-    scene_producer<NP, GRAD, PM, NLL>(a, lay, c);
+    scene_producer<NP, GRAD, PM, NLL, CR>(a, lay, c);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
 }
@@ -1828,6 +1837,12 @@ int scene_step_launch(const StepArgs& a, hipStream_t st) {
     return set_err(G2K_ELDS, "Nmax=%d, stride=%d needs %lld bytes of LDS", a.d.Nmax, a.d.stride,
                    (long long)l.total * 4);
   const int tpw = H / 64;
+  // split scenes: the scene tickets zeroed on the launch stream first (one
+  // 64-byte line per 16 scenes): every launch starts from zero whatever an
+  // earlier launch left (an aborted one, a caller's uninitialised workspace)
+  if (a.scene_ticket &&
+      hipMemsetAsync(a.scene_ticket, 0, (size_t)((a.d.S + 15) / 16) * 64, st) != hipSuccess)
+    return set_err(G2K_ELAUNCH, "scene tickets: memset failed");
   const int rc = grad ? launch_np<true>(a, l, NP, tpw, st) : launch_np<false>(a, l, NP, tpw, st);
   if (rc) return rc;
   return check_launch(grad ? "g2k_scene_kernel (train)" : "g2k_scene_kernel");

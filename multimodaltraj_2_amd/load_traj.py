@@ -139,11 +139,18 @@ class DataLoader:
         self.frame_dict = frame_dict
         if raw_data is not None:
             self._set_raw(np.asarray(raw_data, dtype=np.float64), val=infer)
-        else:
+        elif os.path.isdir(self.current_dir):
             files = sorted(glob.glob(os.path.join(self.current_dir, "*.csv")))
             if not files:
                 raise FileNotFoundError(f"no CSV under {self.current_dir}")
             self.load_dataset(files[int(self.dataset_pointer)], val=infer)
+        else:
+            # a file entry of the list (town_center.csv, annotation_tc.txt):
+            # loaded as is (load_traj.py:89-92); the reference's data/ does not
+            # ship them, so this raises FileNotFoundError as np.genfromtxt does
+            if not os.path.exists(self.current_dir):
+                raise FileNotFoundError(f"{self.current_dir} not found (load_traj.py:89-92)")
+            self.load_dataset(self.current_dir, val=infer)
         self._traj = None          # the frame dict, built on first use
         self.num_batches = int((len(self.frameList) / self.seq_length) / self.batch_size)
 

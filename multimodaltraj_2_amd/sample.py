@@ -78,13 +78,44 @@ def model_weights(restored, n, D, T, seed, device, log=print):
     return w
 
 
-def sample_batch(args, sc, vislet_past, restored, device, seed):
+class StageTimer:
+    """Per-stage wall times of sample.py:256-325 by HIP events on the current
+    stream (the reference's time.time() prints become hipEvent
+    timers): ``mark(name)`` closes the stage running since the previous mark;
+    ``seconds()`` synchronises once and returns {stage: seconds}."""
+
+    def __init__(self, device):
+        self.device = device
+        self.events = []
+        self.t0 = self._event()
+
+    def _event(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def mark(self, name):
+        self.events.append((name, self._event()))
+
+    def seconds(self):
+        self.events[-1][1].synchronize()
+        out, prev = {}, self.t0
+        for name, e in self.events:
+            out[name] = prev.elapsed_time(e) / 1e3
+            prev = e
+        out["total"] = self.t0.elapsed_time(self.events[-1][1]) / 1e3
+        return out
+
+
+def sample_batch(args, sc, vislet_past, restored, device, seed, timer=None):
     """One batch of sample.py (see the module docstring).  Returns
-    (ade, fde, vislet_emb, pred [2, 12, n]) — errors from g2k_ade_fde_f32."""
+    (ade, fde, vislet_emb, pred [2, 12, n]) — errors from g2k_ade_fde_f32.
+    ``timer`` (StageTimer): the stages of sample.py:256-325 are marked on it."""
     D, T = args.num_freq_blocks, args.obs_len
     n = sc.window.shape[1]
     rng = np.random.default_rng(seed)
     tt = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=device)
+    mark = timer.mark if timer is not None else (lambda name: None)
     batch_v = np.linalg.norm(sc.window, axis=2)                     # [obs_len, n]
     weight_i = tt(rng.standard_normal((n, D)))
     weight_ii = tt(rng.standard_normal((D, batch_v.shape[0])))
@@ -95,12 +126,18 @@ def sample_batch(args, sc, vislet_past, restored, device, seed):
                                               num_layers=args.num_layers, grid_size=args.grid_size,
                                               embedding_size=args.embedding_size, device=device,
                                               seed=seed)
-    ng_output, _ = enc.forward(inputs.contiguous(), torch.zeros((D, args.rnn_size), device=device))
     model = g2k_lstm_mcr(in_features=(D, D), hidden_size=args.rnn_size, obs_len=T, num_nodes=n,
                          lambda_reg=args.lambda_param, device=device,
                          weights=model_weights(restored, n, D, T, seed + 1, device))
+    mark("setup")
+    ng_output, _ = enc.forward(inputs.contiguous(), torch.zeros((D, args.rnn_size), device=device))
+    mark("social")                                                  # sample.py:258-268
+    mark("static")                                                  # :273-282 (not run, see main)
+    mark("combined")                                                # :284-291 (not run)
     pred = model.forward(dict(outputs=torch.cat([inputs, vislet_emb], 0), ngh=args.lambda_param * ng_output,
                               rel_features=vislet_rel, out_size=n))
+    mark("predictive")                                              # :300-310
+    mark("relational")                                              # :313-322 (no op in the reference)
     nmax = max(n, 1)
     pr = torch.zeros((1, 2 * fs.PRED_LEN, nmax), device=device)
     pr[0, :, :n] = model.temp_path
@@ -108,12 +145,14 @@ def sample_batch(args, sc, vislet_past, restored, device, seed):
     tg[0, :n] = tt(sc.targets)
     err = fs.ade_fde(pr, tg, torch.tensor([n], dtype=torch.int32, device=device), variant=1,
                      obs_length=args.obs_length)
+    mark("errors")                                                  # :326-330
     e = err[0].cpu().numpy()
     return float(e[0]), float(e[1]), vislet_emb, pred
 
 
 def batches(args, loader):
-    """sample.py:137-164 / 318-320: (scene, targets present) per batch."""
+    """sample.py:137-164 / 318-320: (batch index, scene, the batch's frame
+    dict x_batch) per batch with targets."""
     for b in range(loader.num_batches):
         batch, tgt, _ = loader.next_step()
         if len(batch) == 0:
@@ -128,39 +167,90 @@ def batches(args, loader):
         if y.ndim != 3 or y.shape[1] < fs.PRED_LEN or sc.window.shape[1] < 1:
             continue
         sc.targets = y[:sc.window.shape[1], :fs.PRED_LEN]
-        yield b, sc
+        yield b, sc, batch
+
+
+STAGE_LINES = (   # sample.py:268, 282, 291, 310, 322, 325 (wording kept)
+    ("social", "wall-clock time taken by social mask grid = {0} seconds"),
+    ("static", "wall-clock time taken by static mask grid = {0} seconds"),
+    ("combined", "wall-clock time taken by combined mask grid = {0} seconds"),
+    ("predictive", "wall-clock time taken by predictive kernel = {0} seconds"),
+    ("relational", "Relational inference calculation took= {0} seconds"),
+)
 
 
 def run(args, loader, device, log=print):
+    """sample.py:137-340: every batch, its stage timings (hipEvents), its
+    errors; returns (total, final, results) with results =
+    [(x_batch, complete_traj [n, 12, 2], obs_length)] as sample.py:340 builds it."""
     restored = restore_weights(args.save_dir, device)
     vislet_past = 1.0
-    total, final = [], []
-    for b, sc in batches(args, loader):
-        ade, fde, vislet_past, _ = sample_batch(args, sc, vislet_past, restored, device, args.seed)
+    total, final, results = [], [], []
+    for b, sc, x_batch in batches(args, loader):
+        log("********************** SAMPLING A NEW TRAJECTORY", b,
+            "******************************")
+        timer = StageTimer(device)
+        ade, fde, vislet_past, pred = sample_batch(args, sc, vislet_past, restored, device,
+                                                   args.seed, timer)
+        sec = timer.seconds()
+        for key, line in STAGE_LINES:
+            log(line.format(sec[key]))
+        # start -> end of sample.py:256-325 (the model's stages, not the errors)
+        log("Multi-Cued model (MCR) sampling time = {0} seconds".format(
+            sum(sec[k] for k, _ in STAGE_LINES)))
         total.append(ade)
         final.append(fde)
         log(f"batch {b}: ADE {ade:.4f} FDE {fde:.4f} peds {sc.window.shape[1]}")
-    return total, final
+        log("Processed trajectory number : ", b, "out of ", loader.num_batches, " trajectories")
+        complete_traj = np.transpose(pred.detach().cpu().numpy(), (2, 1, 0))   # sample.py:326
+        results.append((x_batch, complete_traj, args.obs_length))              # :340
+    return total, final, results
 
 
-def main(argv=None):
+def save_results(results, save_dir, log=print):
+    """sample.py:346-348: pickle.dump(results) to <save dir>/social_results.pkl
+    (the reference's hard-coded save directory is --save_dir here, Q8;
+    the current directory without one).  Returns the path."""
+    import pickle
+    log("Saving results")
+    path = os.path.join(save_dir or ".", "social_results.pkl")
+    with open(path, "wb") as f:
+        pickle.dump(results, f)
+    return path
+
+
+def parse_args(argv=None):
+    """argParser.py's flags plus sample.py's own (sample.py:89-106), same
+    names and defaults."""
     base = ArgsParser().parser
     p = argparse.ArgumentParser(parents=[base], add_help=False, conflict_handler="resolve")
     p.add_argument('--obs_length', type=int, default=8)
     p.add_argument('--pred_length', type=int, default=12)
-    p.add_argument('--test_dataset', type=int, default=2)
+    p.add_argument('--test_dataset', type=int, default=5)   # sample.py:98 (5: town_center.csv)
     p.add_argument('--epoch', type=int, default=2)
-    args = p.parse_args(argv)
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse_args(argv)
     device = torch.device(args.device)
+    # dataset 5 is town_center.csv (load_traj.py:30), which the reference's data/
+    # does not ship: the loader raises FileNotFoundError there, as the
+    # reference's np.genfromtxt does
     loader = DataLoader(args, datasets=[0, 1, 2, 3, 4, 5], start=args.test_dataset, sel=0,
                         data_root=args.data_root)
     loader.reset_data_pointer()
     if args.save_dir and not os.path.exists(os.path.join(args.save_dir, "checkpoint")):
         print(f"no checkpoint state file in {args.save_dir}: weights drawn N(0, 1)")
-    total, final = run(args, loader, device)
+    print("static / combined mask grid stages: not run (their outputs feed nothing the "
+          "prediction reads, and the reference's stat_mask [dim, num_freq_blocks] + [8, 1] "
+          "does not broadcast: sample.py:181-182); timed as empty stages")
+    total, final, results = run(args, loader, device)
     if total:
         print("Total mean error of the model is ", np.mean(total))
         print("Total final error of the model is ", np.mean(final))
+    save_results(results, args.save_dir)
+    return total, final, results
 
 
 if __name__ == '__main__':

@@ -51,7 +51,7 @@ def test_sample_d10_restored_matches_oracle(gpu, tmp_path, name):
     D, lam, seed = args.num_freq_blocks, args.lambda_param, args.seed
     past_g, past_o = 1.0, 1.0
     done = 0
-    for b, sc in sample.batches(args, dl):
+    for b, sc, _ in sample.batches(args, dl):
         ade, fde, vis_emb, pred = sample.sample_batch(args, sc, past_g, restored, gpu, seed)
         torch.cuda.synchronize()
         past_g = vis_emb
@@ -82,3 +82,39 @@ def test_sample_d10_restored_matches_oracle(gpu, tmp_path, name):
         if done == 3:
             break
     assert done >= 1
+
+
+def test_sample_run_timings_and_results_pickle(gpu, tmp_path):
+    """sample.py:256-348: every batch prints the per-stage wall times (hipEvent
+    timers here) and the run pickles results = [(x_batch, complete_traj,
+    obs_length)] with complete_traj = pred_path_band transposed (2, 1, 0)
+    (sample.py:326, 340, 346-348)."""
+    import pickle
+    args = _args(_save_dir(tmp_path))
+    z = np.load(os.path.join(GOLDEN, "data_zara01.npz"))
+    dl = DataLoader(args, raw_data=z["raw_data"])
+    dl.reset_data_pointer()
+    dl.num_batches = 3
+    lines = []
+    total, final, results = sample.run(args, dl, gpu, log=lambda *a: lines.append(" ".join(map(str, a))))
+    assert len(results) == len(total) >= 1
+    path = sample.save_results(results, args.save_dir, log=lines.append)
+    assert path == os.path.join(args.save_dir, "social_results.pkl")
+    with open(path, "rb") as f:          # our own file
+        back = pickle.load(f)
+    # the same batches again: pred per batch, to compare with the pickle
+    dl2 = DataLoader(args, raw_data=z["raw_data"])
+    dl2.reset_data_pointer()
+    dl2.num_batches = 3
+    restored = sample.restore_weights(args.save_dir, gpu)
+    past = 1.0
+    for (xb, ct, obs), (b, sc, x_batch) in zip(back, sample.batches(args, dl2)):
+        _, _, past, pred = sample.sample_batch(args, sc, past, restored, gpu, args.seed)
+        assert obs == 8 and list(xb.keys()) == list(x_batch.keys())
+        np.testing.assert_array_equal(ct, np.transpose(pred.cpu().numpy(), (2, 1, 0)))
+        assert ct.shape == (sc.window.shape[1], 12, 2)
+    for key in ("social mask grid", "static mask grid", "combined mask grid", "predictive kernel",
+                "Relational inference calculation took", "Multi-Cued model (MCR) sampling time"):
+        got = [float(l.split("= ")[1].split()[0]) for l in lines if key in l]
+        assert len(got) == len(results) and all(v >= 0 for v in got), key
+    assert sum(1 for l in lines if "SAMPLING A NEW TRAJECTORY" in l) == len(results)

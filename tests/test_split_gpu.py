@@ -8,7 +8,10 @@ one-workgroup launch; the metric sums and the gradient are sums over frames
 whose order changes with X (fixed for a given X: deterministic), so they are
 held to the oracle's tolerances against X = 1 here and to the oracle itself
 in test_step_gpu / test_train_gpu (whose small-S cases run split).  The
-per-scene tickets in the workspace must be re-armed by every call."""
+per-scene tickets in the workspace are zeroed on the stream by every launch
+(ABI 7): a workspace poisoned with arbitrary bytes before any call — a
+caller's uninitialised buffer, an aborted launch's leftovers — must give the
+same results on the first and every later call."""
 import numpy as np
 import pytest
 import torch
@@ -42,7 +45,9 @@ def test_forward_split_equals_one_workgroup(gpu, S, Nmax, H, F, coresident):
                            t["h0"], n_frames=nfr, want_attn=True, pred_layout="ped", split=X,
                            coresident=coresident)
         runs = []
-        for _ in range(3):                     # the tickets are re-armed by every call
+        ws = plan._keep[-1]
+        for i in range(3):                     # every launch zeroes its tickets itself
+            ws.random_(0, 256)                 # poisoned tickets and partials
             o = plan.run()
             torch.cuda.synchronize()
             runs.append({k: getattr(o, k).cpu().numpy().copy() for k in
@@ -51,9 +56,6 @@ def test_forward_split_equals_one_workgroup(gpu, S, Nmax, H, F, coresident):
             for k in r:
                 np.testing.assert_array_equal(r[k], runs[0][k])    # deterministic per X
         outs[X] = runs[0]
-        if X > 1:
-            ws = plan._keep[-1]
-            assert int(ws[:64 * ((S + 15) // 16)].count_nonzero()) == 0   # tickets back at zero
     nf = nfr.cpu().numpy()
     for X in (2, 3, 4):
         for s in range(S):
@@ -84,7 +86,10 @@ def test_train_split_matches_one_workgroup(gpu, S, Nmax, F, loss):
                 np.random.default_rng(1).normal(0.0, 0.3, (3, 12)).astype(np.float32)).to(gpu)
         tp = ts.TrainPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
                           n_frames=nfr, lam=0.05, loss=loss, split=X)
-        g = [tp.run().clone() for _ in range(2)]
+        g = []
+        for _ in range(2):
+            tp._ws.random_(0, 256)            # poisoned rows, tickets and partials
+            g.append(tp.run().clone())
         torch.cuda.synchronize()
         assert torch.equal(g[0], g[1])                                  # deterministic per X
         res[X] = (g[0].double().cpu().numpy(), tp.out.h.cpu().numpy().copy(),
@@ -135,8 +140,6 @@ def test_split_plan_on_a_side_stream_right_after_building(gpu):
         plan.run()
     torch.cuda.synchronize()
     np.testing.assert_array_equal(plan.out.metrics.cpu().numpy(), want.metrics.cpu().numpy())
-    ws = plan._keep[-1]
-    assert int(ws[:64 * ((S + 15) // 16)].count_nonzero()) == 0
     assert fs.step_split(S, F, H, Nmax, t["pos"].shape[1], b.stride) == min(4, 256 // S)
 
 

@@ -233,3 +233,63 @@ def test_train_step_world2_branch_matches_one_rank(gpu, monkeypatch):
     assert np.abs(gn[:P] - gr[:P]).max() <= 1e-5 * np.abs(gr[:P]).max()
     assert gn[P + 1] == gr[P + 1]
     assert np.abs(flat.cpu().numpy() - p1.cpu().numpy()).max() <= 1e-5
+
+
+# The recurrence waves' gradient frames (the last R = 4 own frames of the
+# last chunk once it holds 2 NP or more) split by tile with producers 0..R-1
+# (g2k_scene.hip grad_rec_tiles), checked against the oracle: 3 tiles (an odd
+# split, Nmax 48 with 33+ active), Nmax 256 (dWo^T added in frame order
+# across recurrence waves and producers, dwo_seq), the NLL loss, and H = 512
+# (the 4-producer train build, whose recurrence waves form As but not M of
+# the first frames: the producers publish M only with the cost the gradient
+# terms read).  Through the train step (h_in given: the recurrence runs).
+@pytest.mark.parametrize("Nmax,F,H,loss", [(48, 20, 128, "l2"), (256, 16, 128, "l2"),
+                                           (48, 20, 128, "nll"), (48, 12, 512, "l2"),
+                                           (64, 9, 512, "l2")])
+def test_train_rec_frames_tile_split_matches_oracle(gpu, Nmax, F, H, loss):
+    S = 3
+    n_active = [Nmax, max(Nmax - 5, 33), 17]
+    b = make_batch(S, Nmax, H, F=F, seed=41, n_active=n_active, h0_scale=1.0)
+    nfr = np.array([F, F - 1, F], np.int32)
+    mask = np.ones((S, Nmax), bool)
+    mask[0, 3::7] = False
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    if loss == "nll":
+        params.Wo.mul_(0.05)
+        params.head = torch.from_numpy((0.3 * np.random.default_rng(5).standard_normal((3, 12)))
+                                       .astype(np.float32)).to(gpu)
+    t = b.to_device(gpu)
+    kw = dict(n_frames=torch.from_numpy(nfr).to(gpu),
+              ped_mask=torch.from_numpy(mask.astype(np.uint8)).to(gpu), lam=0.05)
+    tp = ts.TrainPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
+                      loss=loss, **kw)
+    g = tp.run().cpu().numpy().astype(np.float64)
+    w = params.numpy()
+    order = ref.GRAD_ORDER + (("head",) if loss == "nll" else ())
+    R = {k: 0.0 for k in order}
+    lsum = cnt = 0
+    for s in range(S):
+        l_, c_, gg = ref.scene_loss_grad(b.pos[s], b.vislet[s], b.G[s], w, b.targets[s],
+                                         b.n_active[s], n_frames=int(nfr[s]), lam=0.05,
+                                         ped_mask=mask[s], loss=loss, head=w.get("head"))
+        lsum += l_
+        cnt += c_
+        for k in order:
+            R[k] = R[k] + gg[k]
+    off = 0
+    for k in order:
+        r = np.asarray(R[k]).reshape(-1)
+        got = g[off:off + r.size]
+        off += r.size
+        if k == "Wr":
+            assert np.all(got == 0)
+        else:
+            assert np.abs(got - r).max() <= TOL * np.abs(r).max(), k
+    assert off == ts.grad_size(Nmax, loss)
+    assert abs(g[off] - lsum) <= TOL * abs(lsum) and g[off + 1] == cnt
+    # the forward outputs of the same launch: pred and h as the forward step's
+    fwd = fs.step_fused(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
+                        **kw)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(tp.out.pred.cpu().numpy(), fwd.pred.cpu().numpy())
+    np.testing.assert_array_equal(tp.out.h.cpu().numpy(), fwd.h.cpu().numpy())

@@ -1,0 +1,282 @@
+#!/usr/bin/env python3
+"""Golden vectors for the a9 displacement errors, computed by the REFERENCE'S
+OWN statements (this container only; a no-op where /root/reference is absent).
+
+The reference's error code is pure NumPy, but its modules import TensorFlow
+1.x at module level (sample.py:9, train.py), which is absent here.  So the
+statements are taken from the reference's source with ``ast`` at generation
+time — nothing of their text is written to the repository — compiled into
+functions, and executed with real NumPy (no TF, no stand-ins; their prints go
+to /dev/null):
+
+  * get_mean_error                  sample.py:21-82 (the whole function);
+  * the validation frame block      train.py:636-662 (pred_path transpose,
+                                    num_targets, the per-(row, key) loop with
+                                    its short-target branch :642-646);
+  * the per-batch reductions        train.py:668-674 (both the l == 5 and the
+                                    other divisor);
+  * the training-log frame block    train.py:254-276 (raw vectors; rows whose
+                                    pedestrian id is not a target key raise
+                                    KeyError and are skipped).
+
+Inputs are real walk batches of the reference's own data side
+(tools/ref_walks.py drives load_traj.DataLoader.next_step and
+networkx_graph.online_graph): the validation walk from the data seed (target
+dicts as next_step returns them: cumulative, 12 copies per draw) and
+sample.py's walk (fresh graph per batch).  Predictions:
+  * validation / training-log cases: the float64 oracle's forward
+    (oracle/g2k_ref.py frame_forward) of the batch's window with seeded
+    fp32-valued weights, G and the dataset's vislet — so the GPU fused step can
+    be run on the same inputs and its metric terms checked against the
+    reference's own numbers;
+  * get_mean_error cases: seeded N(0, 1) draws (sample.py feeds a random
+    normal as pred_path_band, sample.py:309).
+Extra cases the data never produces: target lists truncated below pred_len
+(the validation short-target branch), observed_length 0 / 5 and
+maxNumPeds < P for get_mean_error (oracle-only cases).
+
+Writes tests/golden/errors_<name>.npz (data only).
+"""
+from __future__ import annotations
+
+import ast
+import contextlib
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "tests", "golden")
+
+DATASETS = {"eth_hotel": "eth/hotel/", "zara01": "ucy/zara/zara01/",
+            "zara02": "ucy/zara/zara02/", "ucy_univ": "ucy/univ/"}
+MAX_VAL = 10          # validation batches per dataset
+MAX_GM = 8            # get_mean_error batches per dataset
+NMAX = 64             # pedestrians per case (node slice: <= 8, Q10; time slice: P)
+PRED_LEN = 12
+
+
+# --------------------------------------------------------------------------
+# The reference's statements as callables (ast, at generation time)
+# --------------------------------------------------------------------------
+def _find(body, lo, hi, out):
+    for st in body:
+        if st.lineno >= lo and st.end_lineno <= hi:
+            out.append(st)
+            continue
+        for fld in ("body", "orelse", "finalbody", "handlers"):
+            sub = getattr(st, fld, None)
+            if isinstance(sub, list):
+                _find(sub, lo, hi, out)
+    return out
+
+
+def ref_block(fname, lo, hi, params, returns):
+    """The statements of /root/reference/<fname> lying wholly in lines lo..hi
+    (one contiguous run of one body) as ``f(**params) -> returns``."""
+    tree = ast.parse(open(os.path.join(REF, fname)).read())
+    stmts = _find(tree.body, lo, hi, [])
+    if not stmts:
+        raise RuntimeError(f"{fname}:{lo}-{hi}: no statements")
+    ret = ast.Return(value=ast.Tuple(elts=[ast.Name(id=r, ctx=ast.Load()) for r in returns],
+                                     ctx=ast.Load()))
+    fn = ast.FunctionDef(name="_blk", args=ast.arguments(
+        posonlyargs=[], args=[ast.arg(arg=p) for p in params], kwonlyargs=[], kw_defaults=[],
+        defaults=[]), body=stmts + [ret], decorator_list=[], returns=None, type_comment=None)
+    mod = ast.fix_missing_locations(ast.Module(body=[fn], type_ignores=[]))
+    ns = {"np": np}
+    exec(compile(mod, f"{REF}/{fname}:{lo}-{hi}", "exec"), ns)
+    return ns["_blk"], [(type(s).__name__, s.lineno, s.end_lineno) for s in stmts]
+
+
+def ref_function(fname, name):
+    tree = ast.parse(open(os.path.join(REF, fname)).read())
+    fn = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == name]
+    mod = ast.fix_missing_locations(ast.Module(body=fn, type_ignores=[]))
+    ns = {"np": np}
+    exec(compile(mod, f"{REF}/{fname}:{name}", "exec"), ns)
+    return ns[name], (fn[0].lineno, fn[0].end_lineno)
+
+
+def quiet(f, *a, **k):
+    with open(os.devnull, "w") as dn, contextlib.redirect_stdout(dn):
+        return f(*a, **k)
+
+
+# --------------------------------------------------------------------------
+# Cases
+# --------------------------------------------------------------------------
+def weights(seed):
+    """fp32-valued N(0, 1) weights in frame_step.init_params' order and shapes."""
+    rng = np.random.default_rng(seed)
+    shapes = [("Wi", (NMAX, 16)), ("Wii", (16, 8)), ("Wv", (8, 18)), ("bv", (16,)),
+              ("Wr", (8, 2)), ("Wc", (24, 8)), ("Wo", (8, NMAX))]
+    w = {k: rng.standard_normal(s).astype(np.float32).astype(np.float64) for k, s in shapes}
+    G = rng.standard_normal((16, 8)).astype(np.float32).astype(np.float64)
+    return w, G
+
+
+def store_dict(td, n):
+    """The part of a target dict the error blocks can read for n rows: the
+    first n keys (insertion order) and every id 1..n-1 that is a key (the
+    training log's ``target_traj[i]``), with their true lengths and first 12
+    points (all a full-length pair reads; short lists are stored whole)."""
+    keys = list(td.keys())
+    keep = keys[:n] + [i for i in range(1, n) if i in td and i not in keys[:n]]
+    lens = np.array([len(td[k]) for k in keep], np.int64)
+    heads = np.full((len(keep), PRED_LEN, 2), np.nan)
+    for j, k in enumerate(keep):
+        t = np.asarray(td[k], np.float64).reshape(-1, 2)[:PRED_LEN]
+        heads[j, :len(t)] = t
+    return np.array(keep, np.int64), lens, heads, len(td)
+
+
+def truncate(td, n, seed):
+    """A copy of the dict with some of the first n keys' lists cut below
+    pred_len (lengths 1..11): the validation short-target branch."""
+    rng = np.random.default_rng(seed)
+    out = {k: list(v) for k, v in td.items()}
+    for j, k in enumerate(list(out)[:n]):
+        if j % 2 == 0 or rng.random() < 0.3:
+            out[k] = out[k][:int(rng.integers(1, PRED_LEN))]
+    return out
+
+
+def make(name, rel, blocks):
+    import make_fixtures as mf
+    sys.path.insert(0, REF)
+    import networkx_graph
+    import load_traj
+    import ref_walks
+    from oracle import g2k_ref as ref
+
+    gm_fn, val_blk, red_blk, tl_blk = blocks
+    args = types.SimpleNamespace(pred_len=PRED_LEN)
+    out = {}
+    seed = sum(map(ord, name))
+    w, G = weights(seed)
+    for k, v in w.items():
+        out["w_" + k] = v.astype(np.float32)
+    out["G"] = G.astype(np.float32)
+
+    # ---- the batches -----------------------------------------------------------
+    # (a) the validation walk from the data seed (train.py:371-445, 556): the
+    #     node slice (Q10) leaves nodes only in a dataset's first batch (Q22);
+    # (b) sample.py's walk (sample.py:138-164): fresh graph, time slice, N = P,
+    #     vislet from column 0 (sample.py:184) — the build's real-data scenes.
+    dl, rargs = mf.ref_loader(rel)
+    load_traj.DataLoader.next_step.__defaults__[0].clear()
+    vrecs, _ = ref_walks.valid_walk(dl, networkx_graph, rargs, dl.seed, keep_targets=True)
+    vis_all = dl.vislet if dl.vislet.shape[0] == 2 else np.zeros((2, dl.vislet.shape[1]))
+    dl, rargs = mf.ref_loader(rel)
+    load_traj.DataLoader.next_step.__defaults__[0].clear()
+    srecs = ref_walks.sample_walk(dl, networkx_graph, rargs, offset=0, max_batches=4 * MAX_VAL,
+                                  keep_targets=True)
+    batches = []
+    for r in vrecs:
+        if int(r.get("n", -1)) >= 1:
+            batches.append(("valid", int(r["n"]), np.asarray(r["window"], np.float64),
+                            int(r["vis_off"]), r["target_traj"], len(r["keys"])))
+    for r in srecs:
+        P = int(r["P"])
+        if 1 <= P <= NMAX:
+            win = np.transpose(np.asarray(r["npl"], np.float64)[:, 0:8], (1, 0, 2))   # [8, P, 2]
+            batches.append(("sample", P, win, 0, r["target_traj"], len(r["keys"])))
+
+    # ---- validation / training-log cases -------------------------------------
+    c = 0
+    for src, n, window, vo, td, nb in batches:
+        if c >= MAX_VAL:
+            break
+        pos = np.zeros((8, NMAX, 2))
+        pos[:, :n] = window[:, :n]
+        pos = pos.astype(np.float32).astype(np.float64)
+        vis = np.zeros((2, NMAX))
+        seg = vis_all[:, vo:vo + n]
+        vis[:, :seg.shape[1]] = seg
+        vis = vis.astype(np.float32).astype(np.float64)
+        fw = ref.frame_forward(pos, vis, G, w, 5e-4, n)
+        band = fw["Y"].reshape(2, PRED_LEN, n)                      # pred_path_band
+        p = f"val{c}_"
+        out[p + "src"] = np.array(src)
+        out[p + "n"], out[p + "nb"] = np.int64(n), np.int64(nb)
+        out[p + "pos"], out[p + "vislet"] = pos.astype(np.float32), vis.astype(np.float32)
+        out[p + "pred"] = band
+        for tag, tdx in (("", td), ("short_", truncate(td, n, seed + c))):
+            keys, lens, heads, K = store_dict(tdx, n)
+            q = p + tag
+            out[q + "keys"], out[q + "lens"], out[q + "heads"], out[q + "K"] = keys, lens, heads, np.int64(K)
+            fde, cv_err = [], []
+            for _ in range(nb):                                     # for frame in batch (:556)
+                quiet(val_blk, band.copy(), n, tdx, args, fde, cv_err, 0)
+            out[q + "cv_err"] = np.array(cv_err, np.float64)
+            out[q + "fde"] = np.array(fde, np.float64).reshape(-1, 2)
+            for l, key in ((2, "b"), (5, "b5")):
+                a, f = [], []
+                quiet(red_blk, cv_err, fde, a, f, l, n, list(range(nb)))
+                out[q + "ade_" + key] = np.float64(a[0] if a else np.nan)
+                out[q + "fde_" + key] = np.float64(f[0] if f else np.nan)
+        # the training-log block (train.py:254-276) on the same batch (full lists)
+        euc, fde = [], []
+        nt = nte = 0
+        for _ in range(nb):
+            nt, nte = quiet(tl_blk, band.copy(), n, td, args, euc, fde, nt, nte)
+        out[p + "tl_euc"] = np.array(euc, np.float64).reshape(-1, PRED_LEN, 2)
+        out[p + "tl_fde"] = np.array(fde, np.float64).reshape(-1, 2)
+        out[p + "tl_num_end_targets"] = np.int64(nte)
+        out[p + "tl_num_targets"] = np.int64(nt)
+        c += 1
+    out["val_count"] = np.int64(c)
+
+    # ---- get_mean_error on sample.py's batches (sample.py:326-330) ------------
+    rng = np.random.default_rng(seed + 1000)
+    g = 0
+    for r in srecs:
+        P = int(r["P"])
+        if P < 1 or g >= MAX_GM or not np.all(r["node_tlens"] == PRED_LEN):
+            continue
+        y = np.asarray(r["node_targets"], np.float64)                # stack(...).squeeze(1) [P, 12, 2]
+        band = rng.standard_normal((2, PRED_LEN, P)).astype(np.float32).astype(np.float64)
+        ct = np.transpose(band, (2, 1, 0))                           # sample.py:326
+        variants = [(8, P)] + ([(0, P), (5, max(P - 1, 1))] if g % 2 == 0 else [])
+        for v, (obs, mp) in enumerate(variants):
+            q = f"gm{g}_{v}_"
+            ade, fde, cnt = quiet(gm_fn, ct.copy(), y.copy(), obs, mp)
+            out[q + "obs"], out[q + "maxped"] = np.int64(obs), np.int64(mp)
+            out[q + "ade"], out[q + "fde"], out[q + "counter"] = np.float64(ade), np.float64(fde), np.int64(cnt)
+        out[f"gm{g}_pred"], out[f"gm{g}_true"] = band, y
+        out[f"gm{g}_variants"] = np.int64(len(variants))
+        g += 1
+    out["gm_count"] = np.int64(g)
+    np.savez_compressed(os.path.join(OUT, f"errors_{name}.npz"), **out)
+    return c, g
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("no /root/reference here: fixtures are committed, nothing to do")
+        return
+    gm_fn, gm_lines = ref_function("sample.py", "get_mean_error")
+    val_blk, v_st = ref_block("train.py", 636, 662,
+                              ["pred_path", "num_nodes", "target_traj", "args", "fde", "cv_err",
+                               "num_targets"], ["num_targets"])
+    red_blk, r_st = ref_block("train.py", 668, 674,
+                              ["cv_err", "fde", "cv_ade_err", "cv_fde_err", "l", "num_nodes", "batch"],
+                              ["cv_ade_err"])
+    tl_blk, t_st = ref_block("train.py", 254, 276,
+                             ["pred_path", "num_nodes", "target_traj", "args", "euc_loss", "fde",
+                              "num_targets", "num_end_targets"], ["num_targets", "num_end_targets"])
+    print("sample.py get_mean_error lines", gm_lines)
+    print("train.py blocks:", v_st, r_st, t_st)
+    for name, rel in DATASETS.items():
+        print(name, "validation cases, get_mean_error cases:",
+              make(name, rel, (gm_fn, val_blk, red_blk, tl_blk)))
+
+
+if __name__ == "__main__":
+    main()

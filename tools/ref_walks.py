@@ -153,9 +153,12 @@ def train_walk(dl, graph_mod, args, epochs):
     return recs, events
 
 
-def valid_walk(dl, graph_mod, args, start_pointer):
+def valid_walk(dl, graph_mod, args, start_pointer, keep_targets=False):
     """train.py:371-445, 556, 681: the validation leg's data side from
-    ``start_pointer`` (the reference: 0, reset_data_pointer(valid=True))."""
+    ``start_pointer`` (the reference: 0, reset_data_pointer(valid=True)).
+    ``keep_targets``: each record also holds a copy of the batch's target dict
+    as next_step returned it (``target_traj``: the default-argument dict
+    shared by every call, load_traj.py:153, so later calls keep growing it)."""
     graph = graph_mod.online_graph(args)                      # :374
     dl.reset_data_pointer(valid=True, frame_pointer=start_pointer)   # :377
     valid_frame_pointer = int((dl.len - int(dl.max * .7)) / dl.val_max)   # :408-409
@@ -175,6 +178,8 @@ def valid_walk(dl, graph_mod, args, start_pointer):
                    keys=np.array(list(batch.keys()), np.float64), node_ids=ids,
                    npl_digest=digest(ids, npl), P=len(ids), vis_off=float(valid_frame_pointer))
         rec.update(_targets_record(target_traj, max_keys=8))
+        if keep_targets:
+            rec["target_traj"] = {k: [list(p) for p in v] for k, v in target_traj.items()}
         bv = list(graph_t.get_node_attr(param="node_pos_list").values())
         if len(bv) == 0:                                      # :434-435
             end = "no_nodes"
@@ -202,11 +207,12 @@ def valid_walk(dl, graph_mod, args, start_pointer):
                       valid_frame_pointer=valid_frame_pointer)
 
 
-def sample_walk(dl, graph_mod, args, offset=0, max_batches=None):
+def sample_walk(dl, graph_mod, args, offset=0, max_batches=None, keep_targets=False):
     """sample.py:125-164 from frame pointer seed + 8*offset: a fresh graph per
     batch, ConstructGraph(framenum=0), time slice.  Stops at the first empty
     batch (sample.py:146-147) or after ``max_batches`` (sample.py runs
-    num_batches)."""
+    num_batches).  ``keep_targets``: each record also holds a copy of the
+    target dict next_step returned (``target_traj``, see valid_walk)."""
     dl.reset_data_pointer()                                   # :125
     dl.frame_pointer += dl.diff * offset
     frame = 0                                                 # :128
@@ -229,5 +235,7 @@ def sample_walk(dl, graph_mod, args, offset=0, max_batches=None):
         recs.append(dict(b=b, fp=fp0, keys=np.array(list(x_batch.keys()), np.float64),
                          node_ids=ids, npl=npl, node_tlens=tl, node_targets=th,
                          P=len(ids)))
+        if keep_targets:
+            recs[-1]["target_traj"] = {k: [list(p) for p in v] for k, v in y_batch.items()}
         b += 1
     return recs
