@@ -268,7 +268,7 @@ def test_step_h512_long_chain_margin(gpu):
     """The split-f16 recurrence product at its widest (H = 512: row sums Z ~
     H, the A operand ~ 128 As log2(e) / Z smallest) over a long chain (F = 100
     frames, nonzero h0): h stays inside close_h's 1e-5 relative bound
-    (DESIGN.md §6 "recurrence numerics": worst-case ~6e-6 per frame at H = 512,
+    (DESIGN.md §6a "Recurrence numerics": worst-case ~6e-6 per frame at H = 512,
     the rounding errors do not compound across frames because every frame
     renormalises).  The measured margin is printed."""
     b, out, res = run_both(2, 32, 512, F=100, device=gpu, h0_scale=1.0)

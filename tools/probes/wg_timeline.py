@@ -19,15 +19,16 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "tools", "ab", "libg2k_timeline.so")
-NREC = 80
+OUT = os.environ.get("TL_OUT", os.path.join(ROOT, "tools", "ab", "libg2k_timeline.so"))
+NREC = 128
 
 DEF = r"""
-__device__ unsigned g2k_tl_buf[8192 * 80];
+__device__ unsigned g2k_tl_buf[8192 * 128];
 __device__ unsigned g2k_tl_ctr;
+// stamps go to a per-workgroup LDS record (no global round trip on the
+// stamped path); the last wave to exit copies the record to g2k_tl_buf
 #define G2K_TL(k, cond) do { if ((cond) && c.lane == 0) { \
-  const int _s = *reinterpret_cast<const int*>(c.sWi - lay.o_wi + lay.total); \
-  g2k_tl_buf[(size_t)_s * 80 + (k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
+  reinterpret_cast<unsigned*>(c.sWi - lay.o_wi + lay.total)[(k)] = (unsigned)__builtin_amdgcn_s_memtime(); } } while (0)
 """
 EXPORT = r"""
 extern "C" int g2k_tl_copy(unsigned* host, int n) {
@@ -41,22 +42,39 @@ extern "C" int g2k_tl_reset(void) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g2k::g2k_tl_ctr), &z, 4, 0, hipMemcpyHostToDevice);
 }
 """
-ENTRY = r"""  if (c.tid == 0) {
+ENTRY = r"""  if (c.wv == 0) {
+    unsigned* r = reinterpret_cast<unsigned*>(smem + lay.total);
     const unsigned t0 = (unsigned)__builtin_amdgcn_s_memtime();
-    const int s_ = (int)(atomicAdd(&g2k_tl_ctr, 1u) & 8191u);   // (wraps: warm-up launches)
-    reinterpret_cast<int*>(smem + lay.total)[0] = s_;
-    unsigned* r = g2k_tl_buf + (size_t)s_ * 80;
-    r[0] = blockIdx.x + 1;
-    r[1] = (unsigned)((uintptr_t)a.h_out >> 8);
-    r[2] = __builtin_amdgcn_s_getreg(63492);
-    r[3] = __builtin_amdgcn_s_getreg(63508);
-    r[4] = t0;
+    for (int k = c.lane; k < 128; k += 64) r[k] = 0u;
+    if (c.lane == 0) {
+      r[0] = blockIdx.x + 1;
+      r[1] = (unsigned)((uintptr_t)a.h_out >> 8);
+      r[2] = __builtin_amdgcn_s_getreg(63492);
+      r[3] = __builtin_amdgcn_s_getreg(63508);
+      r[4] = t0;
+      r[70] = g2k_t_entry;
+    }
   }
 """
+EXIT = r"""  G2K_TL(32 + c.wv, true);
+  if (c.lane == 0) {
+    unsigned* r = reinterpret_cast<unsigned*>(smem + lay.total);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    const unsigned old = atomicAdd(r + 127, 1u);
+    if (old == (unsigned)(NT / 64 - 1)) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const unsigned s_ = atomicAdd(&g2k_tl_ctr, 1u) & 8191u;   // (wraps: warm-up launches)
+      for (int k = 0; k < 127; ++k) g2k_tl_buf[(size_t)s_ * 128 + k] = r[k];
+    }
+  }
+}"""
 REPS = [
+    ("  extern __shared__ __attribute__((aligned(16))) float smem[];\n",
+     "  extern __shared__ __attribute__((aligned(16))) float smem[];\n"
+     "  const unsigned g2k_t_entry = (unsigned)__builtin_amdgcn_s_memtime();\n"),
     ("namespace g2k {\nnamespace {\n\nconstexpr int kSceneChunk",
      "namespace g2k {\n" + DEF + "namespace {\n\nconstexpr int kSceneChunk"),
-    ("  s.total = o;\n  return s;", "  s.total = o + 4;\n  return s;"),
+    ("  const size_t lds = (size_t)l.total * 4;", "  const size_t lds = (size_t)l.total * 4 + 512;   // + the LDS stamp record"),
     ("  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;",
      ENTRY + "  if (c.tid <= kRecW) reinterpret_cast<int*>(c.sRed + 2 * kRB)[c.tid] = 0;"),
     ("  // the first frames' attention weights (E -> A -> As into the ring, the",
@@ -69,8 +87,7 @@ REPS = [
     ("  if (NLL) nll_worker_reduce(c, pw);\n  publish_metrics(a, c, pw,",
      "  G2K_TL(20 + pw, true);\n  if (NLL) nll_worker_reduce(c, pw);\n  publish_metrics(a, c, pw,"),
     ("  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA outlives the workgroup\n}",
-     "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA outlives the workgroup\n"
-     "  G2K_TL(32 + c.wv, true);\n}"),
+     "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA outlives the workgroup\n" + EXIT),
     ("    for (int i = pw; i < nh; i += NP) {",
      "    G2K_TL(48, pw == 0 && fb == 0);\n    int g2k_hk = 0;\n    for (int i = pw; i < nh; i += NP) {"),
     ("        if (lane == 0) lds_store_flag(c.sMflag + fl, f + 1);\n      }\n      __builtin_amdgcn_s_setprio(0);\n    }",
@@ -79,12 +96,15 @@ REPS = [
 ]
 STAGE = [
     ("  __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed\n",
+     "  G2K_TL(96 + c.wv, fb == 0);\n"
      "  __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed\n"
      "  G2K_TL(56 + (c.wv < kRecW ? 0 : 1), (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"),
     ("  __builtin_amdgcn_s_waitcnt(0xc07f);                           // lgkmcnt(0)\n  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2",
      "  G2K_TL(58 + (c.wv < kRecW ? 0 : 1), (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"
      "  G2K_TL(24 + (c.wv - kRecW) % 8, c.wv >= kRecW && c.wv < kRecW + 4 && fb == 0);\n"
-     "  __builtin_amdgcn_s_waitcnt(0xc07f);                           // lgkmcnt(0)\n  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2"),
+     "  __builtin_amdgcn_s_waitcnt(0xc07f);                           // lgkmcnt(0)\n"
+     "  G2K_TL(80 + c.wv, fb == 0);\n"
+     "  __builtin_amdgcn_s_barrier();                                 // B2: V, VG, K1, K2"),
 ]
 PROLOGUE = [
     ("    scene_pos_dma<NT>(a, lay, c, 0, F < lay.fc ? F : lay.fc);   // critical path first\n",
@@ -92,8 +112,8 @@ PROLOGUE = [
      "    G2K_TL(60, c.wv == 0);\n"),
     ("    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)",
      "    G2K_TL(61, c.wv == 0);\n    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)"),
-    ("    scalars();\n    scene_recurrence<TPW, NP>(a, lay, c);",
-     "    scalars();\n    G2K_TL(62, c.wv == 0);\n    scene_recurrence<TPW, NP>(a, lay, c);"),
+    ("    scalars();\n    scene_recurrence<TPW, NP, CR>(a, lay, c);",
+     "    scalars();\n    G2K_TL(62, c.wv == 0);\n    scene_recurrence<TPW, NP, CR>(a, lay, c);"),
     ("  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)\n",
      "  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)\n"
      "  G2K_TL(63, (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"),
@@ -119,13 +139,27 @@ TRAIN += [
      "  if (NLL) nll_worker_reduce(c, NP + c.wv);"),
 ]
 REPS += STAGE + PROLOGUE + TRAIN
+# TL_WARM=1 (build): the first vtile / kmats task of a producer run twice,
+# stamped around each run (is the first run's time the code's first fetch?)
+WARM = [
+    ("      if (task < ntile) {\n        scene_vtile(a, lay, c, 16 * task, wcc);\n      } else {\n        scene_kmats(c);",
+     "      if (task < ntile) {\n        G2K_TL(112 + 3 * task, fb == 0);\n        scene_vtile(a, lay, c, 16 * task, wcc);\n"
+     "        __builtin_amdgcn_s_waitcnt(0xc07f);\n        G2K_TL(113 + 3 * task, fb == 0);\n"
+     "        scene_vtile(a, lay, c, 16 * task, wcc);\n        __builtin_amdgcn_s_waitcnt(0xc07f);\n"
+     "        G2K_TL(114 + 3 * task, fb == 0);\n      } else {\n"
+     "        G2K_TL(118, fb == 0);\n        scene_kmats(c);\n        __builtin_amdgcn_s_waitcnt(0xc07f);\n"
+     "        G2K_TL(119, fb == 0);\n        scene_kmats(c);\n        __builtin_amdgcn_s_waitcnt(0xc07f);\n"
+     "        G2K_TL(120, fb == 0);"),
+]
+if os.environ.get("TL_WARM"):
+    REPS += WARM
 FINE = {48: "heads loop entry", 49: "head 1", 50: "head 2", 51: "head 3", 52: "head 4", 53: "head 5", 54: "head 6", 55: "head 7+"}
 
 
 def build():
     from multimodaltraj_2_amd import build as b
     from concurrent.futures import ThreadPoolExecutor
-    src = os.path.join(ROOT, "multimodaltraj_2_amd", "csrc")
+    src = os.environ.get("TL_SRC", os.path.join(ROOT, "multimodaltraj_2_amd", "csrc"))
     tmp = tempfile.mkdtemp(prefix="g2k_tl_")
     for f in os.listdir(src):
         shutil.copy(os.path.join(src, f), tmp)
@@ -260,8 +294,16 @@ def run(config, nstreams, split=0, cores=False):
           "staged prod0": rel(59) - start, "B2 rec0": rel(5) - start, "chain0": rel(6) - start}
     if np_ == 4:
         print("staging task done per producer (medians):", "  ".join(f"p{p} {np.median(rel(24 + p) - start):.0f}" for p in range(4)))
+    nw = 4 + np_
+    print("B1 arrival per wave (medians):", "  ".join(f"w{w} {np.median(rel(96 + w) - start):.0f}" for w in range(nw)))
+    print("B2 arrival per wave (medians):", "  ".join(f"w{w} {np.median(rel(80 + w) - start):.0f}" for w in range(nw)))
+    if np.any(r[:, 113] != 0):
+        d = lambda i, j: np.median(((r[:, j] - r[:, i]) % (1 << 32))[r[:, j] != 0])   # noqa: E731
+        print(f"warm test: vtile0 first {d(112, 113):.0f} second {d(113, 114):.0f}; "
+              f"vtile1 first {d(115, 116):.0f} second {d(116, 117):.0f}; "
+              f"kmats first {d(118, 119):.0f} second {d(119, 120):.0f}")
     print("lead (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in st.items()))
-    pro = {"pos dma issued": rel(60) - start, "segments issued": rel(61) - start,
+    pro = {"start - entry": (r[:, 4] - r[:, 70]) % (1 << 32), "pos dma issued": rel(60) - start, "segments issued": rel(61) - start,
            "rec0 scalars": rel(62) - start, "loads landed (w0 or p0)": rel(63) - start}
     if os.environ.get("TL_TRAIN"):
         tr = {"heads done": rel(8) - start, "grad frames done": rel(44) - start, "chunk synced": rel(45) - start,
@@ -270,6 +312,11 @@ def run(config, nstreams, split=0, cores=False):
               "flushed": rel(64) - start, "metrics published": rel(65) - start,
               "priv summed": rel(66) - start, "rec0 grad frame done": rel(67) - start}
         print("train, producer 0 (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in tr.items()))
+        ntile = (np.asarray(b.n_active)[(r[:, 0] - 1) % S] + 15) // 16
+        for nt in np.unique(ntile):
+            m = ntile == nt
+            print(f"  scenes with {nt} tile(s) ({m.sum()} wg):", "  ".join(f"{k} {np.median(v[m]):.0f}" for k, v in tr.items()),
+                  f" exit max {(ex - start)[m].max():.0f}")
     print("prologue (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in pro.items()))
     # per XCD: medians / maxima of B1, B2 and the exit (the launch ends with its slowest workgroup)
     b1 = rel(56) - start
