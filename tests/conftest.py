@@ -38,6 +38,8 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from multimodaltraj_2_amd import _lib
+    if os.environ.get("G2K_TEST_LIB"):   # development A/B: a side build (tools/build_lib_variant.sh)
+        _lib._lib = _lib.load(os.environ["G2K_TEST_LIB"])
     _lib.load()   # fails loudly if the HIP library is missing
     return torch.device("cuda:0")
 
