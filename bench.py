@@ -255,11 +255,14 @@ class GraphSteps:
     per-launch cost (Python, the C ABI's checks, hipLaunchKernel) no longer
     paces a ~20 us step.  ``run(i)`` with i a multiple of ``n`` replays it."""
 
-    def __init__(self, step, n, stream, i0=0, side=()):
+    def __init__(self, step, n, stream, i0=0, side=(), thread_local=False):
         self.n = n
         self.g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
-        with torch.cuda.graph(self.g, stream=stream):
+        # thread_local: a capture that holds an RCCL collective (the process
+        # group's watchdog thread keeps querying its events meanwhile)
+        with torch.cuda.graph(self.g, stream=stream,
+                              capture_error_mode="thread_local" if thread_local else "global"):
             for s in side:                     # forked from the capture stream ...
                 s.wait_stream(stream)
             for i in range(n):
@@ -273,11 +276,11 @@ class GraphSteps:
         self.g.replay()
 
 
-def timed_graph(step, n, warmup, dist, sync, stream, side=()):
+def timed_graph(step, n, warmup, dist, sync, stream, side=(), thread_local=False):
     """timed() with the warm-up and the timed steps each as one graph replay
     (exactly ``n`` steps between the barriers)."""
-    gw = GraphSteps(step, max(warmup, 1), stream, side=side)
-    gm = GraphSteps(step, n, stream, i0=max(warmup, 1), side=side)
+    gw = GraphSteps(step, max(warmup, 1), stream, side=side, thread_local=thread_local)
+    gm = GraphSteps(step, n, stream, i0=max(warmup, 1), side=side, thread_local=thread_local)
     gw.replay()
     sync()
     if dist is not None:
@@ -295,6 +298,28 @@ def timed_graph(step, n, warmup, dist, sync, stream, side=()):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         el = float(e.item())
     return el, gm
+
+
+def collective_parts(ts, stream, K, graph, reps=50):
+    """The multi-rank step's parts timed alone with HIP events on the plans'
+    stream (µs each; replayed from a HIP graph of ``reps`` copies when
+    ``graph``, else host launches): gradient (scene kernel + row sum), the
+    all-reduce of the [P + 2] buffer, the update (DESIGN.md §8's budget)."""
+    from multimodaltraj_2_amd.dist import allreduce_grad
+    from multimodaltraj_2_amd.train_step import optimizer_update
+    g = ts.run(0)
+    kw = dict(lr=ts.lr, decay=ts.decay, grad_clip=ts.grad_clip)
+    fns = {"gradient": lambda i: ts._slots[i % K].run(),
+           "allreduce": lambda i: allreduce_grad(g, ts.group, force=True),
+           "update": lambda i: optimizer_update(ts.flat, g, ms=ts.ms, stream=stream, **kw)}
+    parts = {}
+    with torch.cuda.stream(stream):
+        for k, fn in fns.items():
+            if graph:
+                parts[k] = graph_event_time(GraphSteps(fn, reps, stream, thread_local=True), stream)
+            else:
+                parts[k] = event_time(fn, reps, stream)
+    return {k: v * 1e6 for k, v in parts.items()}
 
 
 def graph_event_time(g, stream):
@@ -411,6 +436,13 @@ def main(argv=None):
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from the host instead of replaying the timed steps "
                          "from a HIP graph")
+    ap.add_argument("--collective", choices=("auto", "on"), default="auto",
+                    help="train mode: the multi-rank step structure (gradient -> RCCL all-reduce "
+                         "-> update); auto = when WORLD_SIZE > 1, on = also on one rank (a "
+                         "one-rank nccl group: the structure measured on one GPU)")
+    ap.add_argument("--eager-collective", action="store_true",
+                    help="train mode, collective structure: launch the steps from the host "
+                         "instead of capturing them, all-reduce included, in a HIP graph")
     ap.add_argument("--selftest-launcher", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 
@@ -446,8 +478,12 @@ def main(argv=None):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    if world > 1 or args.collective == "on":
         import torch.distributed as dist
+        if world == 1:                   # a one-rank group (--collective on)
+            for k, v in dict(MASTER_ADDR="127.0.0.1", RANK="0", WORLD_SIZE="1").items():
+                os.environ.setdefault(k, v)
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         dist.init_process_group("nccl", device_id=dev)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
@@ -583,9 +619,10 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
     t0 = batches[0]
     if args.loss == "nll":
         params.head = torch.zeros((3, 12), device=dev)
+    coll = world > 1 or args.collective == "on"
     ts = TrainStep(params, t0["pos"], t0["vislet"], t0["G"], t0["targets"], t0["n_active"],
                    t0["h0"], n_frames=t0["n_frames"], ped_mask=t0["ped_mask"], stride=b.stride,
-                   loss=args.loss, stream=stream, **layout)
+                   loss=args.loss, stream=stream, collective=coll, **layout)
     for t in batches[1:]:
         ts.bind(t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
                 n_frames=t["n_frames"], ped_mask=t["ped_mask"])
@@ -594,17 +631,27 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
     def step(i):
         last["g"] = ts.run(i % K)
 
-    # one rank: one C call per step (gradient + update), replayed from a HIP
-    # graph; across ranks gradient -> all-reduce -> update are enqueued on the
-    # plans' stream with no host wait (eager: the collective is not captured)
-    graph = not args.no_graph and world == 1
+    # one rank: one C call per step (gradient + update); across ranks
+    # gradient -> RCCL all-reduce -> update on the plans' stream.  Either is
+    # replayed from a HIP graph, the collective captured with the kernels
+    # (one eager step first: the communicator and RCCL's own buffers exist
+    # before capture); --eager-collective launches the multi-rank steps from
+    # the host instead
+    graph = not args.no_graph and not (coll and args.eager_collective)
+    in_graph = False
+    if graph and coll:
+        step(0)
+        torch.cuda.synchronize()
     if graph:
-        el, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream)
+        el, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream,
+                             thread_local=coll)
         kern_s = graph_event_time(gm, stream)
+        in_graph = coll
     else:
         el = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
         kern_s = event_time(step, max(20, min(args.steps, 200)), stream)
     gl = last["g"].double().cpu().numpy()
+    parts = collective_parts(ts, stream, K, graph) if coll else None
     abytes = train_algorithmic_bytes(b, H, pbytes, ts.P, layout["targets_shared"])
     achieved = abytes / kern_s / 1e9
     pmc = load_pmc(args.config + "_train")
@@ -613,6 +660,11 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
                       "gradient all-reduce + RMSProp update", "loss": args.loss,
             "value": b.frames * world * args.steps / el, "unit": "frames/s",
             "ms_per_step": el / args.steps * 1e3, "allreduce_bytes": int((ts.P + 2) * 4),
+            "step_structure": ("gradient -> RCCL all-reduce -> update" + (
+                " (HIP graph, collective captured)" if in_graph else " (host launches)"))
+            if coll else "gradient + update in one call (one rank, HIP graph)"
+            if graph else "gradient + update in one call (one rank, host launches)",
+            "collective_parts_us": parts,
             "loss_per_prediction_last_step": float(gl[-2] / max(gl[-1], 1.0)),
             "optimizer": "RMSProp lr 0.005 decay 0.95, global-norm clip 10 (argParser.py:38-47)",
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -42,10 +42,12 @@ def global_errors(tot: torch.Tensor):
     return float(t[0] / cnt), float(torch.sqrt(t[2]) / max(float(t[5]), 1.0))
 
 
-def allreduce_grad(buf: torch.Tensor, group=None) -> torch.Tensor:
+def allreduce_grad(buf: torch.Tensor, group=None, force: bool = False) -> torch.Tensor:
     """Train mode: sum the flat [P + 2] buffer (gradient
     sums, loss, count) over ranks in place — one collective per step; every
-    rank then applies the same update (train_step.TrainStep)."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    rank then applies the same update (train_step.TrainStep).  ``force``
+    issues the collective on a one-rank group too (the multi-rank structure
+    measured and graph-captured on one GPU)."""
+    if dist.is_available() and dist.is_initialized() and (force or dist.get_world_size(group) > 1):
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
     return buf

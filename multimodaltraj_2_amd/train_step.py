@@ -16,6 +16,7 @@ defaults), so the replicas stay identical.  There is no CPU fallback.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import torch
@@ -218,7 +219,7 @@ class TrainStep:
                  lr=LEARNING_RATE, decay=DECAY_RATE, grad_clip=GRAD_CLIP, rmsprop=True,
                  n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None,
                  pred_layout="band", targets_shared=False, frames=None, loss="l2", split=0,
-                 stream=None):
+                 stream=None, collective=None):
         self._layout = dict(pred_layout=pred_layout, targets_shared=targets_shared, frames=frames,
                             loss=loss, split=split, stream=stream)
         self.flat, self.params = flat_params(params, loss)
@@ -228,6 +229,12 @@ class TrainStep:
         self.group = group
         self.world = (dist.get_world_size(group)
                       if dist.is_available() and dist.is_initialized() else 1)
+        # the multi-rank structure (gradient -> all-reduce -> update); True on
+        # one rank forces it (a one-rank group still issues the collective)
+        self.collective = self.world > 1 if collective is None else bool(collective)
+        if self.collective and self.world == 1 and not (dist.is_available()
+                                                        and dist.is_initialized()):
+            raise ValueError("collective=True needs an initialised process group")
         self._lam, self._stride = lam, stride
         self._slots = []
         self.bind(pos, vislet, G, targets, n_active, h, n_frames=n_frames, ped_mask=ped_mask,
@@ -252,16 +259,16 @@ class TrainStep:
         """Returns the (all-rank) [P + 2] buffer: gradient sums, loss, count."""
         plan = self._slots[slot]
         kw = dict(lr=self.lr, decay=self.decay, grad_clip=self.grad_clip)
-        if self.world == 1:                            # nothing to all-reduce: update in the call
+        if not self.collective:                        # nothing to all-reduce: update in the call
             return plan.run(self.flat, self.ms, **kw)
         # gradient -> all-reduce -> update, all enqueued on the plan's stream
         # with no host wait between them: ProcessGroupNCCL orders its RCCL
         # stream after the CURRENT stream and makes the current stream wait
         # for the collective, so the collective is issued with the plan's
         # stream made current (gloo, CPU tests: a host copy inside gloo)
-        s = self._layout["stream"] or torch.cuda.current_stream()
-        with torch.cuda.stream(s):
+        s = self._layout["stream"]
+        with torch.cuda.stream(s) if s is not None else contextlib.nullcontext():
             g = plan.run()
-            allreduce_grad(g, self.group)
+            allreduce_grad(g, self.group, force=True)
             optimizer_update(self.flat, g, ms=self.ms, stream=s, **kw)
         return g

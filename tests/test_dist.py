@@ -121,3 +121,81 @@ def test_two_rank_gloo_gradient_allreduce():
     want = _scene_grads(S, 0, S).numpy()
     for r in range(world):
         np.testing.assert_allclose(got[r], want, rtol=1e-12, atol=1e-12)
+
+
+class _FakePlan:
+    """Stands in for TrainPlan (the HIP launch) on CPU: its gradient buffer is
+    the float64 oracle's [P + 2] for the rank's shard."""
+
+    def __init__(self, grad, log):
+        self.grad, self.log = grad, log
+
+    def run(self, flat=None, ms=None, **kw):
+        assert flat is None            # the collective structure never fuses the update
+        self.log.append("gradient")
+        return self.grad
+
+
+def _structure_worker(rank, world, port, S, steps, q):
+    from multimodaltraj_2_amd import train_step as tsm
+    from oracle import g2k_ref as ref
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_scenes(S, rank, world)
+    log = []
+    P = _scene_grads(S, 0, 1).numel() - 2
+    ts = object.__new__(tsm.TrainStep)            # no HIP library on CPU: the plans are fakes
+    ts.flat = torch.linspace(-1, 1, P, dtype=torch.float64)
+    ts.ms = torch.ones_like(ts.flat)
+    ts.lr, ts.decay, ts.grad_clip = 0.005, 0.95, 10.0
+    ts.group, ts.world, ts.collective = None, world, world > 1
+    ts._layout = dict(stream=None)
+    shard = _scene_grads(S, lo, hi)
+    ts._slots = [_FakePlan(shard.clone(), log)]
+
+    def fake_allreduce(buf, group=None, force=False):
+        log.append("allreduce")
+        return allreduce_grad(buf, group, force)
+
+    def fake_update(flat, grad, *, lr, decay, grad_clip, ms=None, stream=None):
+        log.append("update")
+        p, m = ref.optimizer_update(flat.numpy(), ms.numpy(), grad[:-2].numpy(),
+                                    float(grad[-1]), lr, decay, grad_clip)
+        flat.copy_(torch.from_numpy(p))
+        ms.copy_(torch.from_numpy(m))
+
+    tsm.allreduce_grad, tsm.optimizer_update = fake_allreduce, fake_update
+    for _ in range(steps):
+        ts._slots[0].grad.copy_(shard)
+        ts.run(0)
+    q.put((rank, log, ts.flat.numpy(), ts.ms.numpy()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_train_step_structure():
+    """TrainStep.run across ranks: per step gradient ->
+    ONE all-reduce of the [P + 2] buffer -> update, in that order; every rank
+    ends with the parameters one rank gets from the whole batch's gradient."""
+    from oracle import g2k_ref as ref
+    S, world, steps = 5, 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_structure_worker, args=(r, world, port, S, steps, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, rest) for r, *rest in (q.get(timeout=300) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    g = _scene_grads(S, 0, S).numpy()
+    flat = np.linspace(-1, 1, g.size - 2)
+    ms = np.ones_like(flat)
+    for _ in range(steps):
+        flat, ms = ref.optimizer_update(flat, ms, g[:-2], float(g[-1]), 0.005, 0.95, 10.0)
+    for r in range(world):
+        log, f, m = got[r]
+        assert log == ["gradient", "allreduce", "update"] * steps
+        np.testing.assert_allclose(f, flat, rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(m, ms, rtol=1e-12, atol=1e-14)
