@@ -153,6 +153,24 @@ WARM = [
 ]
 if os.environ.get("TL_WARM"):
     REPS += WARM
+# TL_GRAD=1 (build): producer 0's first two gradient frames of chunk 0, four
+# stamps each (after the M poll, after the first tile, before / after frame_grad)
+GRADF = [
+    ("  for (int fl = f0; fl < fend; fl += fstep) {\n    const int f = fb + fl;\n    const int ford",
+     "  int g2k_gk = 0;\n  for (int fl = f0; fl < fend; fl += fstep) {\n    const int f = fb + fl;\n    const int ford"),
+    ("    poll_flag(c.sMflag + fl, f + 1);                     // M of this frame (a producer's head)\n",
+     "    poll_flag(c.sMflag + fl, f + 1);                     // M of this frame (a producer's head)\n"
+     "    G2K_TL(71 + 4 * g2k_gk, slot == 0 && fb == 0 && t0 == 0 && g2k_gk < 2);\n"),
+    ("                               c.sNllC, c.sNllA + slot * 12 * 64 + c.lane);\n",
+     "                               c.sNllC, c.sNllA + slot * 12 * 64 + c.lane);\n"
+     "      G2K_TL(72 + 4 * g2k_gk, slot == 0 && fb == 0 && t0 == 0 && g2k_gk < 2 && t == t0);\n"),
+    ("    frame_grad(a, lay, c, fl, dm, slot);\n",
+     "    G2K_TL(73 + 4 * g2k_gk, slot == 0 && fb == 0 && t0 == 0 && g2k_gk < 2);\n"
+     "    frame_grad(a, lay, c, fl, dm, slot);\n"
+     "    G2K_TL(74 + 4 * g2k_gk, slot == 0 && fb == 0 && t0 == 0 && g2k_gk < 2);\n    ++g2k_gk;\n"),
+]
+if os.environ.get("TL_GRAD"):
+    REPS += GRADF
 FINE = {48: "heads loop entry", 49: "head 1", 50: "head 2", 51: "head 3", 52: "head 4", 53: "head 5", 54: "head 6", 55: "head 7+"}
 
 
@@ -311,6 +329,13 @@ def run(config, nstreams, split=0, cores=False):
               "prod0 end": rel(20) - start, "chain end": rel(7) - start, "exit": ex - start,
               "flushed": rel(64) - start, "metrics published": rel(65) - start,
               "priv summed": rel(66) - start, "rec0 grad frame done": rel(67) - start}
+        if np.any(r[:, 74] != 0):
+            d = lambda i, j: np.median(((r[:, j] - r[:, i]) % (1 << 32))[(r[:, j] != 0) & (r[:, i] != 0)])   # noqa: E731
+            for g in range(2):
+                o = 71 + 4 * g
+                print(f"producer 0 gradient frame {g}: M ready at {np.median(rel(o) - start):.0f}, first tile {d(o, o + 1):.0f}, "
+                      f"other tiles {d(o + 1, o + 2):.0f}, frame_grad {d(o + 2, o + 3):.0f}"
+                      + (f", to next frame {d(o + 3, o + 4):.0f}" if g == 0 else ""))
         print("train, producer 0 (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in tr.items()))
         ntile = (np.asarray(b.n_active)[(r[:, 0] - 1) % S] + 15) // 16
         for nt in np.unique(ntile):
