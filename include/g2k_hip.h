@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define G2K_ABI_VERSION 7
+#define G2K_ABI_VERSION 8
 
 enum {
   G2K_OK = 0,
@@ -265,6 +265,33 @@ int g2k_gridlstm_f32(const float* in, int64_t ld_in, const float* state, int64_t
                      const float* W, const float* b, const float* peep, float* out,
                      float* state_out, int64_t rows, int32_t blocks, int32_t feature_size,
                      int32_t num_units, void* stream);
+
+/*
+ * g2k_encoder_chain_f32 — --use_grid_lstm (ABI 8): ONE hidden-state chain
+ * through the frames of S batches in order, the vis/loc encoder's
+ * GridLSTMCell in every frame (train.py:197-252 with the encoder stage of
+ * :201-207 taken as st_embeddings; multimodaltraj_2_amd/encoder_step.py).  ONE
+ * workgroup walks the frames (s = 0..S-1, f < n_frames[s]); per frame
+ *   Xe[s][f][:D] = GridLSTMCell(X[s][f][:D], h[:, :D])   (as g2k_gridlstm_f32)
+ *   attn / cost / pred of that frame from Xe[s][f]       (as g2k_mcr_forward_f32)
+ *   h <- one recurrence frame with attn[s][f]            (as g2k_frame_recurrence_f32)
+ * bit-identical to those three calls per frame, without a launch per body.
+ *   d: S, F, T = 8, L = 12, D = 16, H (64..512), Nmax; W, stride, flags 0
+ *   X [S][F][D+2][D], Rel [S][2][D] (g2k_frame_embed_f32), G [S][D][T],
+ *   n_active, n_frames [S] (device; n_frames clamped to [0, F]);
+ *   cell W [fs + 2u][3u], b [3u], peep [4][u] or NULL, feature_size =
+ *   2 num_units (num_units 1, 2, 4: D = 16 columns in, 16 out);
+ *   Xe [S][F][D+2][D] out (X copied first; rows 0..D-1 of the run frames
+ *   replaced); cell_state [D][D] scratch; attn [S][F][D][D], cost
+ *   [S][F][T][T], pred [S][F][2L][Nmax] written for the run frames (others
+ *   untouched); h [D][H] in / out (16-byte aligned, as attn).
+ */
+int g2k_encoder_chain_f32(const g2k_dims* d, const g2k_weights* w, const float* X,
+                          const float* Rel, const float* G, const int32_t* n_active,
+                          const int32_t* n_frames, const float* cell_W, const float* cell_b,
+                          const float* cell_peep, int32_t feature_size, int32_t num_units,
+                          float* Xe, float* cell_state, float* attn, float* cost, float* pred,
+                          float* h, float lambda, void* stream);
 
 /*
  * Train mode (SURVEY.md §8(d) "--mode train", §8(e) gradient all-reduce).  The

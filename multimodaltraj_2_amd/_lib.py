@@ -60,6 +60,9 @@ SYMBOLS = {
     "g2k_eval_rln_ngh_f32": (c_int, [c_vp, c_vp, c_i64, c_i32, c_vp]),
     "g2k_gridlstm_f32": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                                  c_i32, c_i32, c_i32, c_vp]),
+    "g2k_encoder_chain_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32,
+                                      c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp]),
     "g2k_grad_size": (c_i64, [ctypes.POINTER(G2KDims)]),
     "g2k_grad_workspace_bytes": (c_i64, [ctypes.POINTER(G2KDims)]),
     "g2k_step_grad_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
@@ -92,7 +95,7 @@ SYMBOLS = {
                                      c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class G2KLibraryError(RuntimeError):

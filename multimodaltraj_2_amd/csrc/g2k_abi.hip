@@ -340,6 +340,34 @@ int g2k_gridlstm_f32(const float* in, int64_t ld_in, const float* state, int64_t
                          feature_size, num_units, (hipStream_t)stream);
 }
 
+int g2k_encoder_chain_f32(const g2k_dims* d, const g2k_weights* w, const float* X,
+                          const float* Rel, const float* G, const int32_t* n_active,
+                          const int32_t* n_frames, const float* cell_W, const float* cell_b,
+                          const float* cell_peep, int32_t feature_size, int32_t num_units,
+                          float* Xe, float* cell_state, float* attn, float* cost, float* pred,
+                          float* h, float lambda, void* stream) {
+  int rc = validate_common(d, true);
+  if (rc) return rc;
+  if ((rc = validate_weights(w, false))) return rc;
+  if ((rc = validate_H(d->H))) return rc;
+  if (!X || !Rel || !G || !n_active || !n_frames || !cell_W || !cell_b || !Xe || !cell_state ||
+      !attn || !cost || !pred || !h)
+    return set_err(G2K_EINVAL, "a required buffer pointer is NULL");
+  if (!((num_units == 1 && feature_size == 2) || (num_units == 2 && feature_size == 4) ||
+        (num_units == 4 && feature_size == 8)))
+    return set_err(G2K_EUNSUPPORTED,
+                   "num_units=%d feature_size=%d: the encoder maps [D, D] to [D, D] (D = 16) only with "
+                   "feature_size = 2 num_units (built: units 1/2/4)", num_units, feature_size);
+  if (!aligned16(h) || !aligned16(attn)) return set_err(G2K_EINVAL, "h and attn must be 16-byte aligned");
+  if ((int64_t)d->S * d->F == 0) return G2K_OK;
+  const hipStream_t st = (hipStream_t)stream;
+  if (hipMemcpyAsync(Xe, X, (size_t)d->S * d->F * (kD + 2) * kD * sizeof(float),
+                     hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return set_err(G2K_ELAUNCH, "Xe: copy of X failed");
+  return encoder_chain_launch(d, w, X, Rel, G, n_active, n_frames, cell_W, cell_b, cell_peep,
+                              feature_size, num_units, Xe, cell_state, attn, cost, pred, h, lambda, st);
+}
+
 int64_t g2k_grad_size(const g2k_dims* d) {
   if (validate_common(d, false, false, kTrainFlags) != G2K_OK) return -1;
   return grad_params(d->Nmax, loss_nll(*d));

@@ -481,6 +481,11 @@ int errors_launch(const g2k_dims* d, const float* pred, const float* targets,
                   int variant, float* out, hipStream_t st);
 int relation_launch(const float* adj, float* out, int64_t rows, int cols, bool softmax,
                     hipStream_t st);
+int encoder_chain_launch(const g2k_dims* d, const g2k_weights* w, const float* X, const float* Rel,
+                         const float* G, const int32_t* n_active, const int32_t* n_frames,
+                         const float* cell_W, const float* cell_b, const float* cell_peep,
+                         int feature_size, int num_units, float* Xe, float* cell_state, float* attn,
+                         float* cost, float* pred, float* h, float lambda, hipStream_t st);
 int gridlstm_launch(const float* in, int64_t ld_in, const float* state, int64_t ld_state,
                     const float* W, const float* b, const float* peep, float* out, float* state_out,
                     int64_t rows, int blocks, int feature_size, int num_units, hipStream_t st);

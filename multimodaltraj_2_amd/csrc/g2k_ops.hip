@@ -7,6 +7,8 @@
 //   g2k_errors_v0/v1_kernel train.py:636-674 / sample.py:21-82
 //   g2k_sigmoid / g2k_row_softmax  nri_learned.py:16-28
 //   g2k_gridlstm_kernel     helper.py GridLSTMCell encoders (a6)
+//   g2k_encoder_chain_kernel --use_grid_lstm: cell -> forward -> recurrence
+//                           per frame in one workgroup (g2k_encoder_chain_f32)
 //   g2k_ctx_conv / reduce   train.py:92-113, 154-158 static context (a5)
 // D < 16 (sample.py's num_freq_blocks = 10 and the reference checkpoints,
 // SURVEY.md Appendix D) runs on the same 16-wide tiles with the rows and
@@ -54,15 +56,14 @@ __device__ __forceinline__ void attn_row(float* A, int r, int D) {
 // Frame-sequential recurrence, one workgroup per scene, NW waves; the As of
 // up to kRecurChunk frames staged in LDS, h in MFMA registers (g2k_recur.h).
 // ---------------------------------------------------------------------------
+// One scene's chain over F frames (sAs: min(F, kRecurChunk) As tiles; sRed:
+// 4 * 16 * NW floats), the whole workgroup taking part
 template <int TPW, int NW>
-__global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(const float* __restrict__ att,
-                                                            float* __restrict__ h, int F, int D,
-                                                            int H) {
+__device__ __forceinline__ void recur_scene(const float* __restrict__ att, float* __restrict__ h,
+                                            int s, int F, int D, int H, float* sAs, float* sRed) {
   constexpr int kRT = 64 * NW;               // threads
   constexpr int kRB = 16 * NW;               // floats per row-partial buffer
-  __shared__ __attribute__((aligned(16))) float sAs[kRecurChunk * kD * kD];
-  __shared__ __attribute__((aligned(16))) float sRed[4 * kRB];
-  const int s = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int lane = tid & 63, wv = wave_id(), q = lane >> 4, j = lane & 15;
   Recur<TPW, NW> rec;
   float* hs = h + (size_t)s * D * H;
@@ -103,6 +104,15 @@ __global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(const float* __restr
   rec.store(hs, H, wv, q, j, last, D);
 }
 
+template <int TPW, int NW>
+__global__ void __launch_bounds__(64 * NW) g2k_recur_kernel(const float* __restrict__ att,
+                                                            float* __restrict__ h, int F, int D,
+                                                            int H) {
+  __shared__ __attribute__((aligned(16))) float sAs[kRecurChunk * kD * kD];
+  __shared__ __attribute__((aligned(16))) float sRed[4 * 16 * NW];
+  recur_scene<TPW, NW>(att, h, blockIdx.x, F, D, H, sAs, sRed);
+}
+
 // ---------------------------------------------------------------------------
 // g2k_lstm_mcr.forward() only (models/g2k_lstm_mcr.py:99-124), one
 // workgroup per feed, any D <= 16 (row-major [rows][D] operands):
@@ -118,14 +128,14 @@ struct FwdArgs {
   float lambda;
 };
 
-__global__ void __launch_bounds__(kNT) g2k_mcr_forward_kernel(FwdArgs a) {
-  __shared__ float sX[(kD + 2) * kD];
-  __shared__ float sE[kT * kD];
-  __shared__ float sRm[kT * kD];
-  __shared__ float sG[kD * kT];
-  __shared__ float sC[kT * kT];
-  __shared__ float sM[kL2 * kT];
-  const int s = blockIdx.x, tid = threadIdx.x;
+struct FwdLds {
+  float X[(kD + 2) * kD], E[kT * kD], Rm[kT * kD], G[kD * kT], C[kT * kT], M[kL2 * kT];
+};
+
+// feed s of `a` by the whole (kNT-thread) workgroup
+__device__ __forceinline__ void mcr_feed(const FwdArgs& a, int s, FwdLds& l) {
+  float *sX = l.X, *sE = l.E, *sRm = l.Rm, *sG = l.G, *sC = l.C, *sM = l.M;
+  const int tid = threadIdx.x;
   const int Nmax = a.d.Nmax, D = a.d.D;
   const int nact = clampi(a.n_active[s], 0, Nmax);
   for (int i = tid; i < (D + 2) * D; i += kNT) sX[i] = a.X[(size_t)s * (D + 2) * D + i];
@@ -168,6 +178,11 @@ __global__ void __launch_bounds__(kNT) g2k_mcr_forward_kernel(FwdArgs a) {
       for (int t = 0; t < kT; ++t) x = fmaf(sM[jr * kT + t], a.w.Wo[t * Nmax + n], x);
     a.pred[(size_t)s * kL2 * Nmax + i] = x;
   }
+}
+
+__global__ void __launch_bounds__(kNT) g2k_mcr_forward_kernel(FwdArgs a) {
+  __shared__ FwdLds l;
+  mcr_feed(a, blockIdx.x, l);
 }
 
 // ---------------------------------------------------------------------------
@@ -361,9 +376,7 @@ struct GridArgs {
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 template <int U, int FS>
-__global__ void __launch_bounds__(256) g2k_gridlstm_kernel(GridArgs a) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= a.rows) return;
+__device__ __forceinline__ void gridlstm_row(const GridArgs& a, int64_t r) {
   constexpr int NI = FS + 2 * U;
   const float* xr = a.in + r * a.ld_in;
   const float* sr = a.state + r * a.ld_state;
@@ -409,6 +422,68 @@ __global__ void __launch_bounds__(256) g2k_gridlstm_kernel(GridArgs a) {
       orow[2 * U * k + U + j] = mfn;
       cf[j] = cfn;
       mf[j] = mfn;
+    }
+  }
+}
+
+template <int U, int FS>
+__global__ void __launch_bounds__(256) g2k_gridlstm_kernel(GridArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= a.rows) return;
+  gridlstm_row<U, FS>(a, r);
+}
+
+// ---------------------------------------------------------------------------
+// --use_grid_lstm's encoder chain (train.py:197-252 with the encoder stage of
+// :201-207; multimodaltraj_2_amd/encoder_step.py): ONE workgroup walks the
+// frames of S batches in order, per frame the three bodies above — the
+// GridLSTM cell on X[s][f][:D] with h[:, :2uK] as its state (16 lanes, one
+// row each) into Xe, the one-feed forward (attn, cost, pred) from Xe, one
+// recurrence frame on h — separated by workgroup barriers.  The same
+// arithmetic as the three launches per frame (bit-identical), without a
+// launch per body: the chain is latency-bound (one scene's worth of work per
+// frame), so the launches were the cost.  (All global hand-offs stay inside
+// the workgroup: its barriers order them; the CU's vector L1 is shared.)
+// ---------------------------------------------------------------------------
+struct ChainArgs {
+  FwdArgs f;          // d (S = F = 1 per feed), weights, lambda
+  GridArgs g;         // W, b, peep, state = h, state_out (scratch), rows = D, K
+  const float *X, *Rel, *G;
+  const int32_t *n_active, *n_frames;
+  float *Xe, *attn, *cost, *pred, *h;
+  int S, F, H;
+};
+
+template <int TPW, int U, int FS>
+__global__ void __launch_bounds__(kNT) g2k_encoder_chain_kernel(ChainArgs a) {
+  __shared__ FwdLds lf;
+  __shared__ __attribute__((aligned(16))) float sAs[kD * kD];
+  __shared__ __attribute__((aligned(16))) float sRed[4 * 16 * 4];
+  const int Nmax = a.f.d.Nmax;
+  const size_t xrow = (size_t)(kD + 2) * kD;
+  for (int s = 0; s < a.S; ++s) {
+    const int nf = clampi(a.n_frames[s], 0, a.F);
+    for (int f = 0; f < nf; ++f) {
+      const size_t sf = (size_t)s * a.F + f;
+      if (threadIdx.x < kD) {                                     // train.py:201-207
+        GridArgs g = a.g;
+        g.in = a.X + sf * xrow;
+        g.out = a.Xe + sf * xrow;
+        gridlstm_row<U, FS>(g, threadIdx.x);
+      }
+      __syncthreads();
+      FwdArgs w = a.f;                                            // g2k_lstm_mcr.py:99-124
+      w.X = a.Xe + sf * xrow;
+      w.Rel = a.Rel + (size_t)s * 2 * kD;
+      w.G = a.G + (size_t)s * kD * kT;
+      w.n_active = a.n_active + s;
+      w.A_out = a.attn + sf * kD * kD;
+      w.cost_out = a.cost + sf * kT * kT;
+      w.pred = a.pred + sf * kL2 * Nmax;
+      mcr_feed(w, 0, lf);
+      __syncthreads();
+      recur_scene<TPW, 4>(a.attn + sf * kD * kD, a.h, 0, 1, kD, a.H, sAs, sRed);   // :240-252
+      __syncthreads();
     }
   }
 }
@@ -551,6 +626,37 @@ int relation_launch(const float* adj, float* out, int64_t rows, int cols, bool s
   hipLaunchKernelGGL(g2k_sigmoid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, adj,
                      out, n);
   return check_launch("g2k_infer_rlns_f32");
+}
+
+int encoder_chain_launch(const g2k_dims* d, const g2k_weights* w, const float* X, const float* Rel,
+                         const float* G, const int32_t* n_active, const int32_t* n_frames,
+                         const float* cell_W, const float* cell_b, const float* cell_peep,
+                         int feature_size, int num_units, float* Xe, float* cell_state, float* attn,
+                         float* cost, float* pred, float* h, float lambda, hipStream_t st) {
+  ChainArgs a;
+  a.f.d = *d;
+  a.f.d.S = 1; a.f.d.F = 1; a.f.d.H = 64; a.f.d.W = kT; a.f.d.stride = 0; a.f.d.flags = 0;
+  a.f.w = *w; a.f.lambda = lambda;
+  a.g.state = h; a.g.ld_state = d->H; a.g.W = cell_W; a.g.b = cell_b; a.g.peep = cell_peep;
+  a.g.state_out = cell_state; a.g.rows = kD; a.g.ld_in = kD; a.g.K = kD / feature_size;
+  a.X = X; a.Rel = Rel; a.G = G; a.n_active = n_active; a.n_frames = n_frames;
+  a.Xe = Xe; a.attn = attn; a.cost = cost; a.pred = pred; a.h = h;
+  a.S = d->S; a.F = d->F; a.H = d->H;
+#define G2K_CHAIN(T)                                                                            \
+  switch (num_units) {                                                                          \
+    case 1: hipLaunchKernelGGL((g2k_encoder_chain_kernel<T, 1, 2>), dim3(1), dim3(kNT), 0, st, a); break; \
+    case 2: hipLaunchKernelGGL((g2k_encoder_chain_kernel<T, 2, 4>), dim3(1), dim3(kNT), 0, st, a); break; \
+    default: hipLaunchKernelGGL((g2k_encoder_chain_kernel<T, 4, 8>), dim3(1), dim3(kNT), 0, st, a); break; \
+  }
+  switch (d->H / 64) {
+    case 1: G2K_CHAIN(1) break;
+    case 2: G2K_CHAIN(2) break;
+    case 4: G2K_CHAIN(4) break;
+    case 8: G2K_CHAIN(8) break;
+    default: return set_err(G2K_EUNSUPPORTED, "H=%d unsupported", d->H);
+  }
+#undef G2K_CHAIN
+  return check_launch("g2k_encoder_chain_f32");
 }
 
 int gridlstm_launch(const float* in, int64_t ld_in, const float* state, int64_t ld_state,

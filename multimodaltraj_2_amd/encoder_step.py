@@ -14,20 +14,25 @@ model input X = [GridLSTM(inputs, h[:, :16]); vislet_emb] of a frame depends
 on the hidden state and the frames of a chain become sequential (pred and
 attn depend on h, unlike the default path, where only h is a chain).
 
-The chain runs frame by frame on the GPU: g2k_frame_embed_f32 once (every
-frame of every batch), then per frame g2k_gridlstm_f32 (the cell, writing
-straight into that frame's X rows) -> g2k_mcr_forward_f32 (one feed) ->
-g2k_frame_recurrence_f32 (one frame), and g2k_ade_fde_f32 over the collected
-predictions.  There is no CPU fallback.  Oracle: oracle.scene_step(encoder=)
-(gridlstm_cell chained in); the cell is third-party TF contrib code, so its
+The chain runs frame by frame on the GPU in ONE workgroup
+(g2k_encoder_chain_f32, ABI 8): g2k_frame_embed_f32 once (every frame of
+every batch), then a single launch that walks the frames — per frame the
+GridLSTM cell (writing straight into that frame's X rows), the model forward
+of one feed and one recurrence frame, separated by workgroup barriers — and
+g2k_ade_fde_f32 over the collected predictions.  (Round 4 issued three
+launches per frame from a Python loop: tests/test_encoder_chain_gpu.py checks
+both bit-identical and times them.)  There is no CPU fallback.
+Oracle: oracle.scene_step(encoder=) (gridlstm_cell chained in); the cell is
+third-party TF contrib code, so its
 parity is unpinned (row a6)."""
 from __future__ import annotations
 
-import numpy as np
+import ctypes
+
 import torch
 
+from . import _lib
 from . import frame_step as fs
-from .helper import gridlstm
 
 
 class EncoderChain:
@@ -55,25 +60,40 @@ class EncoderChain:
         D, Nmax = fs.HIDDEN_LEN, int(pos.shape[2])
         if tuple(h.shape[:2]) != (1, D) or not h.is_contiguous():
             raise ValueError("h must be one contiguous chain [1, D, H]")
-        nf = n_frames.detach().cpu().numpy().astype(np.int64)
         X, Rel = fs.frame_embed(self.params, pos, vislet, n_active, F, stride=stride,
                                 stream=stream)
-        Xe = X.clone()                      # rows D, D+1 (vislet_emb) stay; 0..D-1 per frame
+        Xe = torch.empty_like(X)            # rows D, D+1 (vislet_emb) = X's; 0..D-1 per frame
         pred = torch.zeros((S, F, 2 * fs.PRED_LEN, Nmax), device=dev)
         attn = torch.zeros((S, F, D, D), device=dev)
         cost = torch.zeros((S, F, fs.OBS_LEN, fs.OBS_LEN), device=dev)
         scratch = torch.empty((D, D), device=dev)
         c = self.cell
-        h0 = h[0]                           # [D, H]: the cell reads its first 16 columns
-        for s in range(S):
-            for f in range(int(nf[s])):
-                gridlstm(X[s, f, :D], h0, c.W, c.b, c.peep, feature_size=c.feature_size,
-                         num_units=c.num_units, out=Xe[s, f, :D], state_out=scratch,
-                         stream=stream)                                       # train.py:201-207
-                fs.mcr_forward(self.params, Xe[s, f:f + 1], Rel[s:s + 1], G[s:s + 1],
-                               n_active[s:s + 1], lam=self.lam, stream=stream,
-                               out=(attn[s, f:f + 1], cost[s, f:f + 1], pred[s, f:f + 1]))
-                fs.frame_recurrence(attn[s:s + 1, f:f + 1], h, stream=stream)   # :240-252
+        for k, t in (("G", G), ("cell W", c.W), ("cell b", c.b)):
+            fs._check_dev(k, t, dev, torch.float32)
+        for k, t in (("n_active", n_active), ("n_frames", n_frames)):
+            fs._check_dev(k, t, dev, torch.int32)
+            if tuple(t.shape) != (S,):
+                raise ValueError(f"{k}: shape {tuple(t.shape)}, expected {(S,)}")
+        if tuple(G.shape) != (S, D, fs.OBS_LEN):
+            raise ValueError(f"G: shape {tuple(G.shape)}, expected {(S, D, fs.OBS_LEN)}")
+        u, fsz = int(c.num_units), int(c.feature_size)
+        if tuple(c.W.shape) != (fsz + 2 * u, 3 * u) or tuple(c.b.shape) != (3 * u,):
+            raise ValueError(f"cell W must be [{fsz + 2 * u}, {3 * u}] and b [{3 * u}]")
+        if c.peep is not None and tuple(c.peep.shape) != (4, u):
+            raise ValueError(f"cell peep must be [4, {u}]")
+        peep = None if c.peep is None else c.peep.contiguous()
+        W, b, Gc = c.W.contiguous(), c.b.contiguous(), G.contiguous()
+        lib = _lib.load()
+        d = _lib.G2KDims(S, F, fs.OBS_LEN, fs.PRED_LEN, D, int(h.shape[2]), Nmax, 0, 0)
+        w = self.params.abi()
+        rc = lib.g2k_encoder_chain_f32(
+            ctypes.byref(d), ctypes.byref(w), fs._ptr(X), fs._ptr(Rel), fs._ptr(Gc),
+            fs._ptr(n_active), fs._ptr(n_frames), W.data_ptr(), b.data_ptr(),
+            None if peep is None else peep.data_ptr(), int(c.feature_size), int(c.num_units),
+            fs._ptr(Xe), fs._ptr(scratch), fs._ptr(attn), fs._ptr(cost), fs._ptr(pred), fs._ptr(h),
+            float(self.lam), fs._stream(stream))                    # train.py:201-207, :240-252
+        _lib.check("g2k_encoder_chain_f32", rc)
+        self._keep = (W, b, peep, Gc, scratch, X, Rel)
         metrics = fs.ade_fde(pred, targets, n_active, n_frames=n_frames, ped_mask=ped_mask,
                              stream=stream)                                   # :636-674
         return fs.StepOutputs(pred=pred, h=h, metrics=metrics, attn=attn, cost=cost), h
