@@ -440,9 +440,10 @@ def main(argv=None):
                     help="train mode: the multi-rank step structure (gradient -> RCCL all-reduce "
                          "-> update); auto = when WORLD_SIZE > 1, on = also on one rank (a "
                          "one-rank nccl group: the structure measured on one GPU)")
-    ap.add_argument("--eager-collective", action="store_true",
-                    help="train mode, collective structure: launch the steps from the host "
-                         "instead of capturing them, all-reduce included, in a HIP graph")
+    ap.add_argument("--capture-collective", action="store_true",
+                    help="train mode, collective structure: capture the steps, RCCL all-reduce "
+                         "included, in one HIP graph (default: host launches; see DESIGN.md §8 "
+                         "for the process-group watchdog race this works around)")
     ap.add_argument("--selftest-launcher", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 
@@ -480,6 +481,11 @@ def main(argv=None):
     dist = None
     if world > 1 or args.collective == "on":
         import torch.distributed as dist
+        if args.capture_collective:
+            # no reuse of ProcessGroupNCCL's cached events across the capture:
+            # its watchdog thread queried a recycled event while a capture
+            # held it (hipErrorCapturedEvent, one run in three)
+            os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
         if world == 1:                   # a one-rank group (--collective on)
             for k, v in dict(MASTER_ADDR="127.0.0.1", RANK="0", WORLD_SIZE="1").items():
                 os.environ.setdefault(k, v)
@@ -631,17 +637,19 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
     def step(i):
         last["g"] = ts.run(i % K)
 
-    # one rank: one C call per step (gradient + update); across ranks
-    # gradient -> RCCL all-reduce -> update on the plans' stream.  Either is
-    # replayed from a HIP graph, the collective captured with the kernels
-    # (one eager step first: the communicator and RCCL's own buffers exist
-    # before capture); --eager-collective launches the multi-rank steps from
-    # the host instead
-    graph = not args.no_graph and not (coll and args.eager_collective)
+    # one rank: one C call per step (gradient + update), replayed from a HIP
+    # graph; across ranks gradient -> RCCL all-reduce -> update on the plans'
+    # stream from host launches, or (--capture-collective) replayed from a HIP
+    # graph with the collective captured beside the kernels (one eager step
+    # first: the communicator and RCCL's own buffers exist before capture;
+    # then a pause so that the process group's watchdog has reaped that
+    # step's work before the capture starts)
+    graph = not args.no_graph and (not coll or args.capture_collective)
     in_graph = False
     if graph and coll:
         step(0)
         torch.cuda.synchronize()
+        time.sleep(0.5)
     if graph:
         el, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream,
                              thread_local=coll)

@@ -1147,8 +1147,8 @@ __device__ __forceinline__ unsigned scene_act_bits(const SceneCtx& c, uint32_t w
 // share shrinks when they have at least two frames each.
 __device__ __forceinline__ int grad_rec_frames(int cnt, int NP) { return cnt >= 2 * NP ? kRecW : 0; }
 // ... split by tile when a frame has two or more: the recurrence wave takes
-// tiles [0, h) (it starts at the chain's end), producer w (w < R, free after
-// its own frames) tiles [h, ntact) of the same frame; each adds its partial
+// tiles [0, h) (it starts at the chain's end), producer NP - R + w (free
+// after its own frames) tiles [h, ntact) of the same frame; each adds its partial
 // dM's weight-side terms (frame_grad is linear in dM) into its own sums
 __device__ __forceinline__ int grad_rec_tiles(int ntact) { return ntact >= 2 ? (ntact + 1) / 2 : ntact; }
 
@@ -1446,7 +1446,10 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     if (GRAD) {
       grad_frames<PM, NLL>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
                            act_bits, acc, lsum, tg[0], true);
-      if (pw < R && grad_rec_tiles(ntact) < ntact) {    // the recurrence waves' frames' other tiles
+      // the recurrence waves' frames' other tiles, to the LAST R producers:
+      // the heads went round-robin from producer 0, so these have one head
+      // fewer (eth_hotel_synth: producers 0-3 three heads, 4-7 two)
+      if (pw < R && grad_rec_tiles(ntact) < ntact) {
         const int fl = own.fo + c.X * (gend + pw);
         grad_frames<PM, NLL>(a, lay, c, pw, fb, fl, 1, fl + 1, act_bits, acc, lsum, tg[0], false,
                              grad_rec_tiles(ntact), ntact);
@@ -1551,10 +1554,17 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       }
     }
   }
-  // the small blocks and dWo, entry by entry over all producer lanes
-  const int ptid = pw * 64 + lane;
+  // the small blocks and dWo, entry by entry over the lanes of the producers
+  // without a dWi tile when those are the majority (Nmax 32: six beside the
+  // two dWi tiles instead of all eight after them, eth_hotel_synth train
+  // 37.8 -> 37.0 us per step; at Nmax 64, four and four, 41.0 -> 41.5: all
+  // producers then, as at every larger Nmax).  Each entry is formed by one
+  // lane in a fixed order, whichever lane: the same values.
+  const int sb0 = 2 * ntile_all < NP ? ntile_all : 0, nsb = NP - sb0;
+  if (pw < sb0) return;
+  const int ptid = (pw - sb0) * 64 + lane;
   #pragma unroll 1
-  for (int p = o_wii + ptid; p < P + 2; p += NP * 64) {
+  for (int p = o_wii + ptid; p < P + 2; p += nsb * 64) {
     float x = 0.f;
     if (p < o_wv) {                                   // dWii[c][u] = sum_t Wv[t][c] AU[t][u]
       const int q2 = p - o_wii, cc = q2 >> 3, uu = q2 & 7;

@@ -6,13 +6,18 @@ replayed.  Both must leave parameters, mean squares and the gradient buffer
 bit-identical to the one-rank fused call (g2k_train_step_f32 with the
 update: the same row sum and update arithmetic in one launch fewer); a
 one-rank all-reduce is the identity.  Then bench.py --collective on runs the
-captured structure end to end.  The N > 1 data path is covered by the gloo
+structure end to end, from host launches (its default) and captured
+(--capture-collective).  Captures run with TORCH_NCCL_CUDA_EVENT_CACHE=0 and
+after a pause that lets the process group's watchdog reap the eager work
+(without them its watchdog once queried a recycled event a capture held:
+hipErrorCapturedEvent).  The N > 1 data path is covered by the gloo
 tests (tests/test_dist.py, tests/test_train_mode*.py); RCCL across GPUs is
 measured by the driver's multi-GPU bench."""
 import json
 import os
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -29,7 +34,7 @@ def _worker(port, q):
     from multimodaltraj_2_amd.synthetic import make_batch
     from multimodaltraj_2_amd.train_step import TrainStep
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
-                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+                      HSA_ENABLE_IPC_MODE_LEGACY="0", TORCH_NCCL_CUDA_EVENT_CACHE="0")
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", device_id=dev)
@@ -51,6 +56,7 @@ def _worker(port, q):
             ge = eager.run()
         graphed.run()                                 # eager: communicator + RCCL buffers
         torch.cuda.synchronize()
+        time.sleep(0.5)                               # (bench.py time_train: watchdog reaps it)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             for _ in range(steps - 1):
@@ -90,18 +96,22 @@ def test_one_rank_rccl_step_structure_bit_identical(gpu):
     np.testing.assert_array_equal(*res["replay2"])
 
 
-def test_bench_collective_structure_captured(gpu):
-    """bench.py --collective on: the train line reports the captured
-    gradient -> all-reduce -> update structure and its parts' times."""
+@pytest.mark.parametrize("capture", [False, True], ids=["host_launches", "captured"])
+def test_bench_collective_structure(gpu, capture):
+    """bench.py --collective on: the train line reports the gradient ->
+    all-reduce -> update structure and its parts' times; host launches by
+    default, one HIP graph with --capture-collective."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--collective", "on", "--steps", "10",
            "--warmup", "3", "--no-cpu-baseline", "--config", "eth_hotel_synth", "--rotate", "4"]
+    if capture:
+        cmd.append("--capture-collective")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     tm = line["train_mode"]
     assert tm["step_structure"].startswith("gradient -> RCCL all-reduce -> update")
-    assert "captured" in tm["step_structure"]
+    assert ("captured" in tm["step_structure"]) == capture
     parts = tm["collective_parts_us"]
     assert set(parts) == {"gradient", "allreduce", "update"} and all(v > 0 for v in parts.values())
-    print(json.dumps({"ms_per_step": tm["ms_per_step"], "parts_us": parts}))
+    print(json.dumps({"capture": capture, "ms_per_step": tm["ms_per_step"], "parts_us": parts}))
