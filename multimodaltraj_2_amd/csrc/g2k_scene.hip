@@ -1147,8 +1147,9 @@ __device__ __forceinline__ unsigned scene_act_bits(const SceneCtx& c, uint32_t w
 // share shrinks when they have at least two frames each.
 __device__ __forceinline__ int grad_rec_frames(int cnt, int NP) { return cnt >= 2 * NP ? kRecW : 0; }
 // ... split by tile when a frame has two or more: the recurrence wave takes
-// tiles [0, h) (it starts at the chain's end), producer NP - R + w (free
-// after its own frames) tiles [h, ntact) of the same frame; each adds its partial
+// tiles [0, h) (it starts at the chain's end), producer w (w < R, free after
+// its own frames; the last R producers measured slower) tiles [h, ntact) of
+// the same frame; each adds its partial
 // dM's weight-side terms (frame_grad is linear in dM) into its own sums
 __device__ __forceinline__ int grad_rec_tiles(int ntact) { return ntact >= 2 ? (ntact + 1) / 2 : ntact; }
 
@@ -1446,10 +1447,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     if (GRAD) {
       grad_frames<PM, NLL>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
                            act_bits, acc, lsum, tg[0], true);
-      // the recurrence waves' frames' other tiles, to the LAST R producers:
-      // the heads went round-robin from producer 0, so these have one head
-      // fewer (eth_hotel_synth: producers 0-3 three heads, 4-7 two)
-      if (pw < R && grad_rec_tiles(ntact) < ntact) {
+      if (pw < R && grad_rec_tiles(ntact) < ntact) {    // the recurrence waves' frames' other tiles
         const int fl = own.fo + c.X * (gend + pw);
         grad_frames<PM, NLL>(a, lay, c, pw, fb, fl, 1, fl + 1, act_bits, acc, lsum, tg[0], false,
                              grad_rec_tiles(ntact), ntact);
