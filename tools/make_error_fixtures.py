@@ -22,7 +22,9 @@ to /dev/null):
 Inputs are real walk batches of the reference's own data side
 (tools/ref_walks.py drives load_traj.DataLoader.next_step and
 networkx_graph.online_graph): the validation walk from the data seed (target
-dicts as next_step returns them: cumulative, 12 copies per draw) and
+dicts as next_step returns them: a fresh dict per call — next_step rebinds
+its empty default argument at the first insertion, load_traj.py:208-209 —
+with each pedestrian's positions appended frame by frame) and
 sample.py's walk (fresh graph per batch).  Predictions:
   * validation / training-log cases: the float64 oracle's forward
     (oracle/g2k_ref.py frame_forward) of the batch's window with seeded

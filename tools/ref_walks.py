@@ -157,8 +157,9 @@ def valid_walk(dl, graph_mod, args, start_pointer, keep_targets=False):
     """train.py:371-445, 556, 681: the validation leg's data side from
     ``start_pointer`` (the reference: 0, reset_data_pointer(valid=True)).
     ``keep_targets``: each record also holds a copy of the batch's target dict
-    as next_step returned it (``target_traj``: the default-argument dict
-    shared by every call, load_traj.py:153, so later calls keep growing it)."""
+    as next_step returned it (``target_traj``: a fresh dict per call —
+    next_step rebinds its empty default argument at the first insertion,
+    load_traj.py:208-209 — so a record's copy is that batch's dict only)."""
     graph = graph_mod.online_graph(args)                      # :374
     dl.reset_data_pointer(valid=True, frame_pointer=start_pointer)   # :377
     valid_frame_pointer = int((dl.len - int(dl.max * .7)) / dl.val_max)   # :408-409
