@@ -174,3 +174,30 @@ def test_context_conv_validates():
     assert lib.g2k_context_conv_f32(p, 576, 720, 5, p, 16, 5e-4, p, None, p, 1 << 30, None) == -4
     assert lib.g2k_context_conv_f32(p, 576, 720, 3, p, 16, 5e-4, None, None, p, 1 << 30, None) == -1
     assert lib.g2k_context_conv_f32(p, 576, 720, 3, p, 16, 5e-4, p, None, p, 16, None) == -1
+
+
+def test_encoder_chain_validates():
+    """g2k_encoder_chain_f32 (ABI 8) rejects bad arguments before any device
+    call; zero frames are a no-op."""
+    lib = _lib.load()
+    w = _lib.G2KWeights(*([ctypes.c_void_p(16)] * 7))
+    p = ctypes.c_void_p(16)
+
+    def call(d, fs=4, u=2, **null):
+        a = dict(X=p, Rel=p, G=p, na=p, nf=p, W=p, b=p, peep=None, Xe=p, cs=p, attn=p, cost=p,
+                 pred=p, h=p)
+        a.update(null)
+        return lib.g2k_encoder_chain_f32(ctypes.byref(d), ctypes.byref(w), a["X"], a["Rel"], a["G"],
+                                         a["na"], a["nf"], a["W"], a["b"], a["peep"], fs, u, a["Xe"],
+                                         a["cs"], a["attn"], a["cost"], a["pred"], a["h"], 0.0005,
+                                         None)
+    assert call(_dims(S=0)) == 0                          # nothing to run
+    assert call(_dims(F=0)) == 0
+    assert call(_dims(H=96)) == -4                        # unsupported hidden size
+    assert call(_dims(D=10)) == -4                        # the chain needs D = 16
+    assert call(_dims(), fs=4, u=1) == -4                 # feature_size must be 2 num_units
+    assert call(_dims(), fs=8, u=3) == -4
+    assert call(_dims(), h=None) == -1                    # required buffers
+    assert call(_dims(), nf=None) == -1
+    assert call(_dims(), h=ctypes.c_void_p(20)) == -1     # h 16-byte aligned
+    assert lib.g2k_last_error()
