@@ -52,10 +52,11 @@ def setup(gpu, S, F, H=128, Nmax=32, seed=5):
     return t, n_frames, G, params, cell, h0
 
 
-@pytest.mark.parametrize("H", [128, 256])
+@pytest.mark.parametrize("H", [64, 128, 256, 512])
 def test_chain_entry_bit_identical_to_python_loop(gpu, H):
     S, F = 5, 7
     t, n_frames, G, params, cell, h0 = setup(gpu, S, F, H=H)
+    n_frames[2] = 0                                   # a batch without frames: skipped
     h_c, h_p = h0.clone(), h0.clone()
     out, _ = EncoderChain(params, cell).run(t["pos"], t["vislet"], G, t["targets"], t["n_active"],
                                             n_frames, h_c, stride=0)
