@@ -125,8 +125,8 @@ TRAIN = [
      "      G2K_TL(45, pw == 0 && fb == 0);\n      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)"),
     ("  grad_priv_sum(c, NP);                                // then all producers see sGAcc",
      "  G2K_TL(46, pw == 0);\n  grad_priv_sum(c, NP);                                // then all producers see sGAcc"),
-    ("  // the small blocks and dWo, entry by entry over all producer lanes",
-     "  G2K_TL(47, pw == 0);\n  // the small blocks and dWo, entry by entry over all producer lanes"),
+    ("  // the small blocks and dWo, entry by entry over the lanes of the producers",
+     "  G2K_TL(47, pw == 0);\n  // the small blocks and dWo, entry by entry over the lanes of the producers"),
 ]
 TRAIN += [
     ("      if (ntact > 0) grad_chunk_flush(a, lay, c, fb, cnt, NP);   // (no active pedestrian: all zero)\n",
@@ -168,6 +168,9 @@ GRADF = [
      "    G2K_TL(73 + 4 * g2k_gk, slot == 0 && fb == 0 && t0 == 0 && g2k_gk < 2);\n"
      "    frame_grad(a, lay, c, fl, dm, slot);\n"
      "    G2K_TL(74 + 4 * g2k_gk, slot == 0 && fb == 0 && t0 == 0 && g2k_gk < 2);\n    ++g2k_gk;\n"),
+    ("      if (pw < R && grad_rec_tiles(ntact) < ntact) {    // the recurrence waves' frames' other tiles\n",
+     "      G2K_TL(121, pw == 0 && fb == 0);\n"
+     "      if (pw < R && grad_rec_tiles(ntact) < ntact) {    // the recurrence waves' frames' other tiles\n"),
 ]
 if os.environ.get("TL_GRAD"):
     REPS += GRADF
@@ -331,11 +334,18 @@ def run(config, nstreams, split=0, cores=False):
               "priv summed": rel(66) - start, "rec0 grad frame done": rel(67) - start}
         if np.any(r[:, 74] != 0):
             d = lambda i, j: np.median(((r[:, j] - r[:, i]) % (1 << 32))[(r[:, j] != 0) & (r[:, i] != 0)])   # noqa: E731
-            for g in range(2):
-                o = 71 + 4 * g
-                print(f"producer 0 gradient frame {g}: M ready at {np.median(rel(o) - start):.0f}, first tile {d(o, o + 1):.0f}, "
-                      f"other tiles {d(o + 1, o + 2):.0f}, frame_grad {d(o + 2, o + 3):.0f}"
-                      + (f", to next frame {d(o + 3, o + 4):.0f}" if g == 0 else ""))
+            ntl = (np.asarray(b.n_active)[(r[:, 0] - 1) % S] + 15) // 16
+            for nt in np.unique(ntl):
+                m = ntl == nt
+                dm_ = lambda i, j: np.median(((r[:, j] - r[:, i]) % (1 << 32))[m & (r[:, j] != 0) & (r[:, i] != 0)])   # noqa: E731
+                for g in range(2):
+                    o = 71 + 4 * g
+                    print(f"  {nt}-tile scenes, producer 0 gradient frame {g}: M ready at {np.median((rel(o) - start)[m]):.0f}, "
+                          f"first tile {dm_(o, o + 1):.0f}, other tiles {dm_(o + 1, o + 2):.0f}, frame_grad {dm_(o + 2, o + 3):.0f}"
+                          + (f", to next frame {dm_(o + 3, o + 4):.0f}" if g == 0 else ""))
+                if np.any(r[m, 121] != 0):
+                    print(f"  {nt}-tile scenes, producer 0: own frames done at {np.median((rel(121) - start)[m]):.0f}, "
+                          f"with the recurrence frames' other tiles at {np.median((rel(44) - start)[m]):.0f}")
         print("train, producer 0 (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in tr.items()))
         ntile = (np.asarray(b.n_active)[(r[:, 0] - 1) % S] + 15) // 16
         for nt in np.unique(ntile):
