@@ -533,8 +533,10 @@ def main(argv=None):
     if args.no_graph:
         elapsed = timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
     else:
+        # (a process group is up: its watchdog thread queries events while we
+        # capture, so the capture is thread-local)
         elapsed, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream,
-                                  side=streams[1:])
+                                  side=streams[1:], thread_local=dist is not None)
     # reference mode: replicas only; the ADE/FDE numerators of the last batch
     # are summed across ranks once at the end
     tot = plans[(args.steps - 1) % K].out.metrics.double().sum(dim=0)
@@ -548,7 +550,8 @@ def main(argv=None):
     if args.no_graph:
         kern_s = event_time(lambda i: one[i % len(one)].run(), R, stream)
     else:
-        kern_s = graph_event_time(GraphSteps(lambda i: one[i % len(one)].run(), R, stream), stream)
+        kern_s = graph_event_time(GraphSteps(lambda i: one[i % len(one)].run(), R, stream,
+                                             thread_local=dist is not None), stream)
     achieved = abytes / kern_s / 1e9
 
     train = None
@@ -652,7 +655,7 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
         time.sleep(0.5)
     if graph:
         el, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream,
-                             thread_local=coll)
+                             thread_local=dist is not None)
         kern_s = graph_event_time(gm, stream)
         in_graph = coll
     else:
