@@ -743,6 +743,7 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
                                           int t, int L, int q, float acc[5], float& lsum,
                                           f32x4 (&dm)[2], f32x4& dWoT, AfterTargets after_targets,
                                           const float* nllC = nullptr, float* nllA = nullptr) {
+  if (GRAD && NLL) asm volatile("" : "+v"(L), "+v"(q));   // (as in frame_grad<OPAQUE>)
   const int n0 = 16 * t, n = n0 + L;
   const bool hi = q < 2;                                   // block-1 rows exist (r < 24)
   f32x4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
@@ -943,6 +944,7 @@ __device__ __forceinline__ f32x4 mm16(FA fa, FB fb, int L, int q) {
 //   dWc_f[r][u] = sum_t dM[r][t] cost[u][t]
 //   dK1_f[t][j] = sum_d dE[t][d] Uaug[j][d]        (E = K1 @ Uaug, j < 10)
 //   dUaug_f[j][d] = sum_t K1[t][j] dE[t][d]        (j < 8: window rows, 8-9: Ve, 10: bv)
+template <bool OPAQUE>
 __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout& lay,
                                            const SceneCtx& c, int fl, const f32x4 (&dm)[2],
                                            int slot) {
@@ -960,7 +962,15 @@ __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout&
   const float* dM = c.sGFrame + slot * kGFrame + kGT_DM;
   float* pacc = c.sGPriv + slot * kGAccFixed;
   float* pdv = c.sGPdV + slot * lay.wcmax * kD + fl * a.d.stride * kD;
-  const int L = c.L, q = c.q, L7 = L & 7, q1 = q & 1;
+  // OPAQUE (the NLL builds): the lane indices made opaque per call, so its
+  // LDS addresses are formed here, not hoisted into the producer's preheader
+  // and held across the whole role — the NLL kernels' register peak
+  // (spill-free then: eth_hotel_synth NLL train 56.3 -> 52.6 us per step;
+  // the L2 builds, with registers to spare, lose 3 us to the re-formed
+  // addresses: DESIGN.md §11)
+  int L = c.L, q = c.q;
+  if (OPAQUE) asm volatile("" : "+v"(L), "+v"(q));
+  const int L7 = L & 7, q1 = q & 1;
   const float* sm = c.sm;
   const float* cost = c.sCost + fl * kT * kT;
   const int wrow0 = fl * a.d.stride;
@@ -1256,7 +1266,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
         if (q < 2) dMs[mrow(16 + 4 * q + v) * kT + L] = dm[1][v];
       }
     }
-    frame_grad(a, lay, c, fl, dm, slot);
+    frame_grad<NLL>(a, lay, c, fl, dm, slot);
     dm[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     dm[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
