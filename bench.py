@@ -267,25 +267,15 @@ def upload_graph(g, stream):
     torch.cuda.synchronize()
 
 
-def _graph_nodes(graph):
-    """A graph's node handles (hipGraphGetNodes; with several streams in a
-    capture its order is not the insertion order)."""
-    import ctypes
-    cnt = ctypes.c_size_t(0)
-    _hip_ok(hip().hipGraphGetNodes(graph, None, ctypes.byref(cnt)), "hipGraphGetNodes")
-    nodes = (ctypes.c_void_p * cnt.value)()
-    _hip_ok(hip().hipGraphGetNodes(graph, nodes, ctypes.byref(cnt)), "hipGraphGetNodes")
-    return [nodes[i] for i in range(cnt.value)]
-
-
 def _capture_nodes(stream):
-    """Node handles of the graph being captured on ``stream`` so far."""
+    """Nodes in the graph being captured on ``stream`` so far."""
     import ctypes
-    st, graph = ctypes.c_int(0), ctypes.c_void_p()
+    st, graph, n = ctypes.c_int(0), ctypes.c_void_p(), ctypes.c_size_t(0)
     _hip_ok(hip().hipStreamGetCaptureInfo_v2(ctypes.c_void_p(stream.cuda_stream), ctypes.byref(st),
                                              None, ctypes.byref(graph), None, None),
             "hipStreamGetCaptureInfo_v2")
-    return set(_graph_nodes(graph))
+    _hip_ok(hip().hipGraphGetNodes(graph, None, ctypes.byref(n)), "hipGraphGetNodes")
+    return n.value
 
 
 _WORK_NODES = (0, 1, 2)          # hipGraphNodeTypeKernel, Memcpy, Memset
@@ -298,14 +288,15 @@ class GraphSteps:
     per-launch cost (Python, the C ABI's checks, hipLaunchKernel) no longer
     paces a ~20 us step.  ``run(i)`` with i a multiple of ``n`` replays it.
     With ``per_step`` the graph's work nodes (kernels, memsets, copies) are
-    grouped by the step that captured them (the nodes the capture gained
-    during that step), so ``replay_only(steps)`` can run a subset of the
-    steps through the same executable (the others disabled for that replay)."""
+    grouped by the step that captured them (the capture's node count after
+    every step; the runtime lists a graph's nodes in insertion order), so
+    ``replay_only(steps)`` can run a subset of the steps through the same
+    executable (the others disabled for that replay)."""
 
     def __init__(self, step, n, stream, i0=0, side=(), thread_local=False, per_step=False):
         self.n = n
         self.g = torch.cuda.CUDAGraph(keep_graph=per_step)
-        seen = []
+        bounds = []
         torch.cuda.synchronize()
         # thread_local: a capture that holds an RCCL collective (the process
         # group's watchdog thread keeps querying its events meanwhile)
@@ -315,29 +306,34 @@ class GraphSteps:
                 s.wait_stream(stream)
             for i in range(n):
                 if per_step:
-                    seen.append(_capture_nodes(stream))
+                    bounds.append(_capture_nodes(stream))
                 step(i0 + i)
             if per_step:
-                seen.append(_capture_nodes(stream))
+                bounds.append(_capture_nodes(stream))
             for s in side:                     # ... and joined back
                 stream.wait_stream(s)
         torch.cuda.synchronize()
         if per_step:
             self.g.instantiate()
-            self._group(seen)
+            self._group(bounds)
         upload_graph(self.g, stream)
 
-    def _group(self, seen):
+    def _group(self, bounds):
         import ctypes
-        nodes = _graph_nodes(ctypes.c_void_p(self.g.raw_cuda_graph()))
-        work = set()
-        for nd in nodes:
+        graph = ctypes.c_void_p(self.g.raw_cuda_graph())
+        cnt = ctypes.c_size_t(0)
+        _hip_ok(hip().hipGraphGetNodes(graph, None, ctypes.byref(cnt)), "hipGraphGetNodes")
+        nodes = (ctypes.c_void_p * cnt.value)()
+        _hip_ok(hip().hipGraphGetNodes(graph, nodes, ctypes.byref(cnt)), "hipGraphGetNodes")
+        work = []
+        for i in range(cnt.value):
             t = ctypes.c_int(-1)
-            _hip_ok(hip().hipGraphNodeGetType(ctypes.c_void_p(nd), ctypes.byref(t)),
+            _hip_ok(hip().hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(t)),
                     "hipGraphNodeGetType")
             if t.value in _WORK_NODES:
-                work.add(nd)
-        self.step_nodes = [sorted((seen[j + 1] - seen[j]) & work) for j in range(self.n)]
+                work.append(i)
+        self.step_nodes = [[nodes[i] for i in work if bounds[j] <= i < bounds[j + 1]]
+                           for j in range(self.n)]
         if sum(map(len, self.step_nodes)) != len(work) or not all(self.step_nodes):
             raise RuntimeError("graph nodes do not group by step")
 
