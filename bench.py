@@ -230,55 +230,22 @@ def event_time(step, reps, stream):
 _HIP = None
 
 
-def hip():
-    """torch's own HIP runtime (libamdhip64 is matched by name to the copy
-    torch loaded: one runtime in the process) with the graph calls typed."""
-    global _HIP
-    if _HIP is None:
-        import ctypes
-        c = ctypes
-        h = c.CDLL("libamdhip64.so")
-        for name, args in (("hipGraphUpload", [c.c_void_p, c.c_void_p]),
-                           ("hipStreamGetCaptureInfo_v2", [c.c_void_p, c.POINTER(c.c_int), c.c_void_p,
-                                                           c.POINTER(c.c_void_p), c.c_void_p, c.c_void_p]),
-                           ("hipGraphGetNodes", [c.c_void_p, c.c_void_p, c.POINTER(c.c_size_t)]),
-                           ("hipGraphNodeGetType", [c.c_void_p, c.POINTER(c.c_int)]),
-                           ("hipGraphNodeSetEnabled", [c.c_void_p, c.c_void_p, c.c_uint])):
-            getattr(h, name).argtypes = args
-            getattr(h, name).restype = c.c_int
-        _HIP = h
-    return _HIP
-
-
-def _hip_ok(rc, what):
-    if rc != 0:
-        raise RuntimeError(f"{what} failed: hipError {rc}")
-
-
 def upload_graph(g, stream):
     """hipGraphUpload of a captured graph's executable on ``stream`` (its
     one-time device-side setup, done at capture time instead of inside the
     first timed replay; runs no step).  G2K_BENCH_NO_UPLOAD=1 skips it (A/B)."""
+    global _HIP
     if os.environ.get("G2K_BENCH_NO_UPLOAD"):
         return
     import ctypes
-    _hip_ok(hip().hipGraphUpload(ctypes.c_void_p(g.raw_cuda_graph_exec()),
-                                 ctypes.c_void_p(stream.cuda_stream)), "hipGraphUpload")
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+        _HIP.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        _HIP.hipGraphUpload.restype = ctypes.c_int
+    rc = _HIP.hipGraphUpload(ctypes.c_void_p(g.raw_cuda_graph_exec()), ctypes.c_void_p(stream.cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"hipGraphUpload failed: {rc}")
     torch.cuda.synchronize()
-
-
-def _capture_nodes(stream):
-    """Nodes in the graph being captured on ``stream`` so far."""
-    import ctypes
-    st, graph, n = ctypes.c_int(0), ctypes.c_void_p(), ctypes.c_size_t(0)
-    _hip_ok(hip().hipStreamGetCaptureInfo_v2(ctypes.c_void_p(stream.cuda_stream), ctypes.byref(st),
-                                             None, ctypes.byref(graph), None, None),
-            "hipStreamGetCaptureInfo_v2")
-    _hip_ok(hip().hipGraphGetNodes(graph, None, ctypes.byref(n)), "hipGraphGetNodes")
-    return n.value
-
-
-_WORK_NODES = (0, 1, 2)          # hipGraphNodeTypeKernel, Memcpy, Memset
 
 
 class GraphSteps:
@@ -286,17 +253,11 @@ class GraphSteps:
     stream): ``n`` consecutive calls of ``step(i0 + i)`` captured once, then
     one graph launch runs all of them back to back on the GPU — the host's
     per-launch cost (Python, the C ABI's checks, hipLaunchKernel) no longer
-    paces a ~20 us step.  ``run(i)`` with i a multiple of ``n`` replays it.
-    With ``per_step`` the graph's work nodes (kernels, memsets, copies) are
-    grouped by the step that captured them (the capture's node count after
-    every step; the runtime lists a graph's nodes in insertion order), so
-    ``replay_only(steps)`` can run a subset of the steps through the same
-    executable (the others disabled for that replay)."""
+    paces a ~20 us step.  ``run(i)`` with i a multiple of ``n`` replays it."""
 
-    def __init__(self, step, n, stream, i0=0, side=(), thread_local=False, per_step=False):
+    def __init__(self, step, n, stream, i0=0, side=(), thread_local=False):
         self.n = n
-        self.g = torch.cuda.CUDAGraph(keep_graph=per_step)
-        bounds = []
+        self.g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
         # thread_local: a capture that holds an RCCL collective (the process
         # group's watchdog thread keeps querying its events meanwhile)
@@ -305,97 +266,22 @@ class GraphSteps:
             for s in side:                     # forked from the capture stream ...
                 s.wait_stream(stream)
             for i in range(n):
-                if per_step:
-                    bounds.append(_capture_nodes(stream))
                 step(i0 + i)
-            if per_step:
-                bounds.append(_capture_nodes(stream))
             for s in side:                     # ... and joined back
                 stream.wait_stream(s)
         torch.cuda.synchronize()
-        if per_step:
-            self.g.instantiate()
-            self._group(bounds)
         upload_graph(self.g, stream)
-
-    def _group(self, bounds):
-        import ctypes
-        graph = ctypes.c_void_p(self.g.raw_cuda_graph())
-        cnt = ctypes.c_size_t(0)
-        _hip_ok(hip().hipGraphGetNodes(graph, None, ctypes.byref(cnt)), "hipGraphGetNodes")
-        nodes = (ctypes.c_void_p * cnt.value)()
-        _hip_ok(hip().hipGraphGetNodes(graph, nodes, ctypes.byref(cnt)), "hipGraphGetNodes")
-        work = []
-        for i in range(cnt.value):
-            t = ctypes.c_int(-1)
-            _hip_ok(hip().hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(t)),
-                    "hipGraphNodeGetType")
-            if t.value in _WORK_NODES:
-                work.append(i)
-        self.step_nodes = [[nodes[i] for i in work if bounds[j] <= i < bounds[j + 1]]
-                           for j in range(self.n)]
-        if sum(map(len, self.step_nodes)) != len(work) or not all(self.step_nodes):
-            raise RuntimeError("graph nodes do not group by step")
-
-    def _enable(self, nodes, on):
-        import ctypes
-        ex = ctypes.c_void_p(self.g.raw_cuda_graph_exec())
-        for nd in nodes:
-            _hip_ok(hip().hipGraphNodeSetEnabled(ex, ctypes.c_void_p(nd), int(on)),
-                    "hipGraphNodeSetEnabled")
-
-    def replay_only(self, steps):
-        """One replay running only the captured steps at positions ``steps``."""
-        off = [nd for j in range(self.n) if j not in set(steps) for nd in self.step_nodes[j]]
-        self._enable(off, False)
-        try:
-            self.g.replay()
-            torch.cuda.synchronize()
-        finally:
-            self._enable(off, True)
 
     def replay(self):
         self.g.replay()
 
 
-def warm_passes(w, n, i0, rotate):
-    """Positions of the timed graph's steps (``step(i0 + j)``, j < n) to run
-    as the ``w`` warm-up steps: the same inputs ``step(0 .. w-1)`` would use
-    (input batch = step index mod ``rotate``), one position per step, split
-    into replays of at most one use per position."""
-    need = [i % rotate for i in range(w)]
-    passes = []
-    while need:
-        used, left = set(), []
-        for b in need:
-            j = next((j for j in range(n) if j not in used and (i0 + j) % rotate == b), None)
-            if j is None and not any((i0 + k) % rotate == b for k in range(n)):
-                j = next((j for j in range(n) if j not in used), None)   # input never timed
-            if j is None:
-                left.append(b)
-            else:
-                used.add(j)
-        passes.append(sorted(used))
-        need = left
-    return passes
-
-
-def timed_graph(step, n, warmup, dist, sync, stream, side=(), thread_local=False, rotate=None):
-    """timed() with the timed steps as one graph replay (exactly ``n`` steps
-    between the barriers).  The warm-up runs ``warmup`` steps through the
-    SAME executable (replays with only those steps' nodes enabled), so the
-    timed replay is not the executable's first; G2K_BENCH_WARM=graph warms
-    with a separate graph of the warm-up steps instead (the earlier form: its
-    timed replay pays the executable's first-launch cost)."""
-    i0 = max(warmup, 1)
-    if os.environ.get("G2K_BENCH_WARM", "exec") == "graph" or warmup == 0:
-        gw = GraphSteps(step, max(warmup, 1), stream, side=side, thread_local=thread_local)
-        gm = GraphSteps(step, n, stream, i0=i0, side=side, thread_local=thread_local)
-        gw.replay()
-    else:
-        gm = GraphSteps(step, n, stream, i0=i0, side=side, thread_local=thread_local, per_step=True)
-        for p in warm_passes(warmup, n, i0, rotate or (i0 + n)):
-            gm.replay_only(p)
+def timed_graph(step, n, warmup, dist, sync, stream, side=(), thread_local=False):
+    """timed() with the warm-up and the timed steps each as one graph replay
+    (exactly ``n`` steps between the barriers)."""
+    gw = GraphSteps(step, max(warmup, 1), stream, side=side, thread_local=thread_local)
+    gm = GraphSteps(step, n, stream, i0=max(warmup, 1), side=side, thread_local=thread_local)
+    gw.replay()
     sync()
     if dist is not None:
         dist.barrier()
@@ -650,7 +536,7 @@ def main(argv=None):
         # (a process group is up: its watchdog thread queries events while we
         # capture, so the capture is thread-local)
         elapsed, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream,
-                                  side=streams[1:], thread_local=dist is not None, rotate=K)
+                                  side=streams[1:], thread_local=dist is not None)
     # reference mode: replicas only; the ADE/FDE numerators of the last batch
     # are summed across ranks once at the end
     tot = plans[(args.steps - 1) % K].out.metrics.double().sum(dim=0)
@@ -707,10 +593,7 @@ def main(argv=None):
                                                                 cores),
                        "streams": len(streams),
                        "launch": "host launch per step" if args.no_graph else
-                                 "HIP graph of the timed steps (one replay)" + (
-                                     "; warm-up through a separate graph"
-                                     if os.environ.get("G2K_BENCH_WARM") == "graph" else
-                                     "; warm-up = W of its steps through the same executable")},
+                                 "HIP graph of the timed steps (one replay)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc[0], "traffic_source": pmc[1],
@@ -772,7 +655,7 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
         time.sleep(0.5)
     if graph:
         el, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream,
-                             thread_local=dist is not None, rotate=K)
+                             thread_local=dist is not None)
         kern_s = graph_event_time(gm, stream)
         in_graph = coll
     else:

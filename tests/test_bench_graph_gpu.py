@@ -65,33 +65,3 @@ def test_graph_event_time_positive(gpu):
     dt = bench.graph_event_time(g, streams[0])
     # one 64-scene launch: microseconds, not the replay's host call alone
     assert 1e-6 < dt < 1e-3
-
-
-@pytest.mark.parametrize("nstreams", [1, 2])
-def test_replay_only_runs_the_chosen_steps(gpu, nstreams):
-    """bench.py's warm-up replays the timed graph with only W steps' nodes
-    enabled (bench.timed_graph): exactly those steps' outputs are written,
-    the others untouched; the next full replay runs every step again."""
-    streams = [torch.cuda.Stream(device=gpu) for _ in range(nstreams)]
-    plans = _plans(gpu, streams)
-    K = len(plans)
-    for p in plans:
-        p.run()
-    torch.cuda.synchronize()
-    eager = [p.out.h.clone() for p in plans]
-    g = bench.GraphSteps(lambda i: plans[i % K].run(), K, streams[0], side=streams[1:],
-                         per_step=True)
-    assert [len(n) for n in g.step_nodes] == [1] * K      # one scene-kernel node per step
-    for p in plans:
-        p.out.h.fill_(float("nan"))
-    torch.cuda.synchronize()
-    g.replay_only([1, 2])
-    for k, p in enumerate(plans):
-        if k in (1, 2):
-            assert torch.equal(p.out.h, eager[k])
-        else:
-            assert torch.isnan(p.out.h).all()
-    g.replay()
-    torch.cuda.synchronize()
-    for p, h in zip(plans, eager):
-        assert torch.equal(p.out.h, h)
