@@ -41,11 +41,26 @@ constexpr int SM_WR = 288;    // [8][2]
 constexpr int SM_WC = 304;    // [24][8]
 constexpr int SM_G = 496;     // [16][8]  G (lambda applied at use)
 // weight-derived matrices (frame head): K1 = [Wv16 @ Wii | Wv[:,16] | Wv[:,17] | 1 | 0]
-// ([8][12]), K2 = Wc @ K1 ([24][12])
+// ([8][12]), K2 = Wc @ K1 ([24][12]).  PAD (the forward kernels, whose LDS
+// has room): stored zero-padded to the 16 lanes of an MFMA operand — K1 as
+// [16][kKP] (rows 8..15 zero), K2 as [32][kKP] (x rows 0..11 at 0..11, y rows
+// 12..23 at 16..27, rows 12..15 and 28..31 zero) — with lambda G as [16][kGP]
+// (columns 8..15 zero), so that the frame heads load every operand straight
+// (no clamped index, no select per operand).  The pitches keep those loads
+// free of bank conflicts (the clamped reads they replace were broadcasts):
+// 18 L mod 32 takes the 16 even residues, so the half-wave's (L, q < 2) words
+// 18 L + q fall in 32 distinct banks; lambda G is read 16 bytes per lane, and
+// 20 L mod 32 puts eight lanes' four-bank groups apart.  The train kernels
+// keep the dense [8][12] / [24][12] form (their LDS is at the 160 KB limit).
 constexpr int SM_K1 = 640;
-constexpr int SM_K2 = 752;
-constexpr int SM_SPARE = 1084;  // write-only word (stores of lanes without an entry)
-constexpr int kSceneSmall = 1088;
+constexpr int kKP = 18, kGP = 20;
+template <bool PAD> struct SmallBlock {
+  static constexpr int K2 = PAD ? SM_K1 + 16 * kKP : 752;
+  static constexpr int LG = SM_K1 + 48 * kKP;      // (PAD only; 16-byte aligned)
+  static constexpr int SPARE = PAD ? LG + 16 * kGP : 1084;   // write-only word (stores of lanes without an entry)
+  static constexpr int size = SPARE + 4;
+};
+static_assert(SmallBlock<false>::size == 1088 && SmallBlock<true>::LG % 4 == 0, "small block");
 constexpr int kKA = 12;       // augmented contraction length (8 window rows + Ve0, Ve1, bv, 0)
 constexpr int kYP = 17;       // train: per-producer dY tile scratch [24][kYP] (pitch: bank spread)
 // global stores per prediction tile: pred_path_band (4-byte path) / pedestrian-major (16-byte)
@@ -86,8 +101,9 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_wo = o;    o += rup4(kT * Nmax);
   s.o_vis = o;   o += rup4(2 * Nmax);                  // vislet rows
   s.o_mask = o;  o += rup4((Nmax + 3) / 4);            // the scene's ped_mask row (LDS-DMA, dword rows)
-  s.o_v = o;     o += rup4((s.wcmax + 2) * kD);        // V rows: window, Ve0, Ve1
-  s.o_small = o; o += kSceneSmall;
+  const bool pad = !grad;                              // (SmallBlock<PAD>: the frame heads' operands)
+  s.o_v = o;     o += pad ? (s.wcmax + 4) * kD : rup4((s.wcmax + 2) * kD);   // V rows: window, Ve0, Ve1 (PAD: bv, 0)
+  s.o_small = o; o += pad ? SmallBlock<true>::size : SmallBlock<false>::size;
   const int NG = NP + kRecW;                          // train: producers + recurrence waves
   s.o_y = o;     o += grad ? NG * kL2 * kYP : 0;      // dY tile scratch (train)
   s.o_met = o;   o += (grad ? NG : NP) * 8;
@@ -97,7 +113,9 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   s.o_mflag = o; o += rup4(fc);                      // M ring flags (prediction tiles poll)
   s.o_red = o;   o += 4 * 16 * kRecW;
   s.o_pos = o;   o += s.wcmax * s.pp;                  // raw position window (LDS-DMA)
-  s.o_vg = o;    o += rup4((s.wcmax + 3) * kT);       // VG = V @ g: window, Ve0, Ve1, bv rows
+  // VG = V @ g: window, Ve0, Ve1, bv rows [.][8] (PAD: [.][16], columns 8..15
+  // zero, and a zero row)
+  s.o_vg = o;    o += pad ? (s.wcmax + 4) * kD : rup4((s.wcmax + 3) * kT);
   s.wtot = (F > 0 ? F - 1 : 0) * stride + kT;
   s.dwo_seq = (int64_t)(NP + kRecW) * Nmax * kT * 4 > 32 * 1024 ? 1 : 0;
   s.o_cost = s.o_gframe = s.o_gpriv = s.o_gpdv = s.o_gacc = s.o_gdv = s.o_gdwo = s.o_gseq = o;
@@ -237,48 +255,73 @@ __device__ __forceinline__ void attn_weights(const f32x4 aA, float* as_dst, int 
 // A contracts over t = 4q + ks (rows of E as the MFMA left them).  As goes
 // to `as_dst`; cost to `cost_g` (global, krnl_mdl.cost) and / or `cost_l`
 // (LDS, train mode); the x / y row tiles of M^T are returned (M[L][4q+i]).
+template <bool PAD>
 __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float* sV,
                                                    const float* sVG, int wrow0, int wcmax,
                                                    const float (&rm)[4], float lam, float* as_dst,
                                                    int* as_flag, int flag_val, float* A_g,
                                                    float* cost_g, float* cost_l, int L, int q,
                                                    bool want_m = true, bool want_as = true) {
-  // every operand load is unconditional (clamped addresses) and issued
-  // before the first MFMA; the lanes' selects follow (an exec-masked load
-  // would cost its own LDS round trip on the chain)
-  const int L7 = L & 7, Lx = L < kL ? L : 0, q2 = q < 2 ? q : 1;
-  float ka[3], ua[3], va[3], bx[3], by[3], gA[4], ub, vb;
+  // every operand load is unconditional and issued before the first MFMA.
+  // PAD: the LDS operands are zero-padded to the 16 lanes (K1, K2, lambda G,
+  // VG columns; the augmented rows Ve0, Ve1, bv, 0 of V and VG), so no lane
+  // selects anything.  Otherwise clamped addresses, the lanes' selects after
+  // (an exec-masked load would cost its own LDS round trip on the chain).
+  using SB = SmallBlock<PAD>;
+  float ka[3], ua[3], va[3], bx[3], by[3], gA[4];
+  if constexpr (PAD) {
 #pragma unroll
-  for (int ks = 0; ks < 3; ++ks) {
-    const int k = 4 * ks + q;
-    ka[ks] = sm[SM_K1 + L7 * kKA + k];
-    bx[ks] = sm[SM_K2 + Lx * kKA + k];
-    by[ks] = sm[SM_K2 + (kL + Lx) * kKA + k];
-    if (ks < 2) {
-      ua[ks] = sV[(wrow0 + k) * kD + L];
-      va[ks] = sVG[(wrow0 + k) * kT + L7];
-    } else {
-      ua[ks] = sV[(wcmax + q2) * kD + L];
-      va[ks] = sVG[(wcmax + (q < 3 ? q : 2)) * kT + L7];   // Ve0, Ve1, bv rows
+    for (int ks = 0; ks < 3; ++ks) {
+      const int k = 4 * ks + q;
+      ka[ks] = sm[SM_K1 + L * kKP + k];
+      bx[ks] = sm[SB::K2 + L * kKP + k];
+      by[ks] = sm[SB::K2 + (16 + L) * kKP + k];
+      const int row = ks < 2 ? wrow0 + k : wcmax + q;   // window rows, then Ve0, Ve1, bv, 0
+      ua[ks] = sV[row * kD + L];
+      va[ks] = sVG[row * kD + L];
     }
-  }
-  ub = sm[SM_BV + L];
+    {
+      const float4 g = *reinterpret_cast<const float4*>(sm + SB::LG + L * kGP + 4 * q);   // lambda g[r = L][t]
+      gA[0] = g.x; gA[1] = g.y; gA[2] = g.z; gA[3] = g.w;
+    }
+    asm volatile("" : "+v"(ka[0]), "+v"(ka[1]), "+v"(ka[2]), "+v"(ua[0]), "+v"(ua[1]), "+v"(ua[2]),
+                 "+v"(va[0]), "+v"(va[1]), "+v"(va[2]));
+    asm volatile("" : "+v"(bx[0]), "+v"(bx[1]), "+v"(bx[2]), "+v"(by[0]), "+v"(by[1]), "+v"(by[2]),
+                 "+v"(gA[0]), "+v"(gA[1]), "+v"(gA[2]), "+v"(gA[3]));
+  } else {
+    const int L7 = L & 7, Lx = L < kL ? L : 0, q2 = q < 2 ? q : 1;
+    float ub;
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) gA[ks] = sm[SM_G + L * kT + 4 * q2 + ks];   // g[r = L][t]
-  asm volatile("" : "+v"(ka[0]), "+v"(ka[1]), "+v"(ka[2]), "+v"(ua[0]), "+v"(ua[1]), "+v"(ua[2]),
-               "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(ub));
-  asm volatile("" : "+v"(bx[0]), "+v"(bx[1]), "+v"(bx[2]), "+v"(by[0]), "+v"(by[1]), "+v"(by[2]),
-               "+v"(gA[0]), "+v"(gA[1]), "+v"(gA[2]), "+v"(gA[3]));
-  (void)vb;
+    for (int ks = 0; ks < 3; ++ks) {
+      const int k = 4 * ks + q;
+      ka[ks] = sm[SM_K1 + L7 * kKA + k];
+      bx[ks] = sm[SB::K2 + Lx * kKA + k];
+      by[ks] = sm[SB::K2 + (kL + Lx) * kKA + k];
+      if (ks < 2) {
+        ua[ks] = sV[(wrow0 + k) * kD + L];
+        va[ks] = sVG[(wrow0 + k) * kT + L7];
+      } else {
+        ua[ks] = sV[(wcmax + q2) * kD + L];
+        va[ks] = sVG[(wcmax + (q < 3 ? q : 2)) * kT + L7];   // Ve0, Ve1, bv rows
+      }
+    }
+    ub = sm[SM_BV + L];
 #pragma unroll
-  for (int ks = 0; ks < 3; ++ks) {
-    ka[ks] = L < kT ? ka[ks] : 0.f;
-    bx[ks] = L < kL ? bx[ks] : 0.f;
-    by[ks] = L < kL ? by[ks] : 0.f;
-    va[ks] = L < kT ? va[ks] : 0.f;
+    for (int ks = 0; ks < 4; ++ks) gA[ks] = sm[SM_G + L * kT + 4 * q2 + ks];   // g[r = L][t]
+    asm volatile("" : "+v"(ka[0]), "+v"(ka[1]), "+v"(ka[2]), "+v"(ua[0]), "+v"(ua[1]), "+v"(ua[2]),
+                 "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(ub));
+    asm volatile("" : "+v"(bx[0]), "+v"(bx[1]), "+v"(bx[2]), "+v"(by[0]), "+v"(by[1]), "+v"(by[2]),
+                 "+v"(gA[0]), "+v"(gA[1]), "+v"(gA[2]), "+v"(gA[3]));
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      ka[ks] = L < kT ? ka[ks] : 0.f;
+      bx[ks] = L < kL ? bx[ks] : 0.f;
+      by[ks] = L < kL ? by[ks] : 0.f;
+      va[ks] = L < kT ? va[ks] : 0.f;
+    }
+    ua[2] = q < 2 ? ua[2] : (q == 2 ? ub : 0.f);
+    va[2] = q == 3 ? 0.f : va[2];
   }
-  ua[2] = q < 2 ? ua[2] : (q == 2 ? ub : 0.f);
-  va[2] = q == 3 ? 0.f : va[2];
   // the recurrence's operand first: E -> A -> As, the As flag; M (only the
   // prediction tiles need it) after, so its six MFMAs do not hold up As.
   // (want_as false: the frame's As comes from a recurrence wave; want_m
@@ -293,7 +336,7 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
     for (int i = 0; i < 4; ++i) em[i] = eN[i] * rm[i];                    // rm = 0 for t >= 8
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
-      aA = mfma4(q < 2 ? lam * gA[ks] : 0.f, em[ks], aA);                 // A[4q+i][L]
+      aA = mfma4(PAD ? gA[ks] : (q < 2 ? lam * gA[ks] : 0.f), em[ks], aA);   // A[4q+i][L]
     __builtin_amdgcn_sched_barrier(0);
     attn_weights(aA, as_dst, L, q);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // As stored before its flag
@@ -375,6 +418,7 @@ __device__ __forceinline__ void scene_pos_dma(const StepArgs& a, const SceneLayo
 // pseudo-row (VG only).  V^T = Wi^T @ N^T over n (k = 4 ks + q), then
 // VG^T = (lambda G)^T @ V^T over d with V^T straight from the registers.
 // Lane (L, q) ends with V[r][4q..4q+3] and VG[r][4q..4q+3] (q < 2).
+template <bool PAD>
 __device__ __forceinline__ void scene_vtile(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int w0, int wcc) {
   // branch-free: every lane loads at clamped addresses and selects, so the
@@ -430,13 +474,21 @@ __device__ __forceinline__ void scene_vtile(const StepArgs& a, const SceneLayout
   const int row = win ? r : lay.wcmax + (r - wcc);               // storage row
   if (win || vis)
     *reinterpret_cast<float4*>(c.sV + row * kD + 4 * q) = make_float4(vt[0], vt[1], vt[2], vt[3]);
-  if ((win || vis || bvrow) && q < 2)
+  if (PAD) {
+    if (win || vis || bvrow)   // (lane groups 2, 3: the zero columns 8..15)
+      *reinterpret_cast<float4*>(c.sVG + row * kD + 4 * q) =
+          q < 2 ? make_float4(vg[0], vg[1], vg[2], vg[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  } else if ((win || vis || bvrow) && q < 2) {
     *reinterpret_cast<float4*>(c.sVG + row * kT + 4 * q) = make_float4(vg[0], vg[1], vg[2], vg[3]);
+  }
 }
 
 // K1 = [Wv[:, :16] @ Wii | Wv[:, 16] | Wv[:, 17] | 1 | 0] ([8][12]) and
 // K2 = Wc @ K1 ([24][12]) by MFMA in one wave (weights only; see frame_head).
+// PAD: stored zero-padded (SmallBlock; the zero rows: scene_pad_consts).
+template <bool PAD>
 __device__ __forceinline__ void scene_kmats(const SceneCtx& c) {
+  using SB = SmallBlock<PAD>;
   const int L = c.L, q = c.q, L7 = L & 7;
   const float* sm = c.sm;
   float av[4], bw[4];
@@ -480,13 +532,55 @@ __device__ __forceinline__ void scene_kmats(const SceneCtx& c) {
     ka = mfma4(wc0[ks], k1[ks], ka);                               // K2[4q + i][L]
     kb = mfma4(wc1[ks], k1[ks], kb);                               // K2[16 + 4q + i][L]
   }
-  // unconditional stores: lanes without an entry write the spare word
+  // unconditional stores: lanes without an entry write the spare word.  PAD:
+  // K1 rows 8..15 are the zeros of lane groups 2, 3; K2 row r goes to r (x
+  // rows, r < 12) or r + 4 (y rows)
+  if constexpr (!PAD) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 4 * q + i;
+      c.sm[L < kKA && q < 2 ? SM_K1 + t * kKA + L : SB::SPARE] = k1[i];
+      c.sm[L < kKA ? SB::K2 + t * kKA + L : SB::SPARE] = ka[i];
+      c.sm[L < kKA && 16 + t < kL2 ? SB::K2 + (16 + t) * kKA + L : SB::SPARE] = kb[i];
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int t = 4 * q + i;
-    c.sm[L < kKA && q < 2 ? SM_K1 + t * kKA + L : SM_SPARE] = k1[i];
-    c.sm[L < kKA ? SM_K2 + t * kKA + L : SM_SPARE] = ka[i];
-    c.sm[L < kKA && 16 + t < kL2 ? SM_K2 + (16 + t) * kKA + L : SM_SPARE] = kb[i];
+    c.sm[L < kKA ? SM_K1 + t * kKP + L : SB::SPARE] = k1[i];
+    c.sm[L < kKA ? SB::K2 + (t < kL ? t : t + 4) * kKP + L : SB::SPARE] = ka[i];
+    c.sm[L < kKA && 16 + t < kL2 ? SB::K2 + (20 + t) * kKP + L : SB::SPARE] = kb[i];
+  }
+}
+
+// PAD: the frame heads' zero-padded operands that are not K1 / K2 values, in
+// one wave of the first staging (a task of its own: beside K1 / K2, not
+// after them) — K2's zero rows 12..15 and 28..31, the scene's lambda G
+// ([16][16], columns 8..15 zero), the augmented operands' constant rows: V
+// row wcmax + 2 = bv, V and VG rows wcmax + 3 = 0 (no chunk's staging writes
+// those rows, so once per scene).
+__device__ __forceinline__ void scene_pad_consts(const SceneCtx& c, const SceneLayout& lay,
+                                                 float lambda) {
+  using SB = SmallBlock<true>;
+  const int L = c.L, q = c.q;
+  const float* sm = c.sm;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = c.lane + 64 * j, r = idx / kKA;
+    if (idx < 8 * kKA) c.sm[SB::K2 + (r < 4 ? kL + r : 24 + r) * kKP + idx % kKA] = 0.f;
+  }
+  // lambda G: lane (L, q) writes row L, columns 4q .. 4q + 3 (zero for q >= 2)
+  {
+    const float4 g = *reinterpret_cast<const float4*>(sm + SM_G + L * kT + 4 * (q & 1));
+    *reinterpret_cast<float4*>(c.sm + SB::LG + L * kGP + 4 * q) =
+        q < 2 ? make_float4(lambda * g.x, lambda * g.y, lambda * g.z, lambda * g.w)
+              : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (q < 3) {
+    float* dst = q == 0 ? c.sV + (lay.wcmax + 2) * kD : q == 1 ? c.sV + (lay.wcmax + 3) * kD
+                                                                : c.sVG + (lay.wcmax + 3) * kD;
+    dst[L] = q == 0 ? sm[SM_BV + L] : 0.f;
   }
 }
 
@@ -544,7 +638,7 @@ __device__ __forceinline__ int rec_head_frames(const SceneLayout& lay, const Sce
 // vmcnt(0) before the first LDS read after the staging — which drained the
 // first tiles' target loads, issued to fly under the frame heads, and held
 // the first head back by a full HBM round trip.)
-template <int NT, int NP, bool NLL = false, typename RecInit>
+template <int NT, int NP, bool PAD, bool NLL = false, typename RecInit>
 __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int fb, int cnt, RecInit rec_init) {
   const int wcc = (cnt - 1) * a.d.stride + kT;
@@ -552,13 +646,15 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
   __builtin_amdgcn_s_barrier();                                 // B1: window + weights landed
   if (c.wv >= kRecW) {
     const int ntile = (wcc + 3 + 15) / 16;
-    const int ntask = ntile + (fb == 0 ? 1 : 0);
+    const int ntask = ntile + (fb == 0 ? (PAD ? 2 : 1) : 0);
     for (int task = c.wv - kRecW; task < ntask; task += NP) {
       if (task < ntile) {
-        scene_vtile(a, lay, c, 16 * task, wcc);
-      } else {
-        scene_kmats(c);
+        scene_vtile<PAD>(a, lay, c, 16 * task, wcc);
+      } else if (!PAD || task == ntile) {
+        scene_kmats<PAD>(c);
         if (NLL) scene_nll_consts(c);
+      } else {
+        if constexpr (PAD) scene_pad_consts(c, lay, a.lambda);
       }
     }
   } else {
@@ -574,7 +670,7 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
 // HBM burst, which every wave's B1 waits for, stays free of it) and its
 // softmax numerators are formed there too; after B2 the waves form As of the
 // first frames themselves and start the chain.
-template <int TPW, int NP, bool CR>
+template <int TPW, int NP, bool CR, bool PAD>
 __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneLayout& lay,
                                                  const SceneCtx& c) {
   constexpr int NT = 64 * (kRecW + NP);
@@ -590,7 +686,7 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   // the staging
   if (live && c.nf > 0) rc.load(a.h_in + (size_t)c.s * kD * H, H, c.wv, c.q, c.L);   // (in the prologue's burst)
   if (c.nf > 0)
-    scene_stage<NT, NP>(a, lay, c, 0, c.nf < lay.fc ? c.nf : lay.fc, [&] {
+    scene_stage<NT, NP, PAD>(a, lay, c, 0, c.nf < lay.fc ? c.nf : lay.fc, [&] {
       if (!live) return;
       rc.init_max(c.sRed + 3 * kRB, c.wv, c.q, c.L);
       asm volatile("" ::: "memory");
@@ -616,7 +712,7 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     // be published before that cost is in LDS
     constexpr bool kRecM = CR;
     const FrameHeadOut hd =
-        frame_head(c.sm, c.sV, c.sVG, fl * a.d.stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
+        frame_head<PAD>(c.sm, c.sV, c.sVG, fl * a.d.stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                    c.sFlag + fl, fl + 1,
                    a.A_out && mine ? a.A_out + ((size_t)c.s * a.d.F + fl) * kD * kD : nullptr,
                    kRecM && a.cost_out && mine ? a.cost_out + ((size_t)c.s * a.d.F + fl) * kT * kT : nullptr,
@@ -636,7 +732,7 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) {
       scene_pos_dma<NT>(a, lay, c, fb, cnt);
-      scene_stage<NT, NP>(a, lay, c, fb, cnt, [] {});
+      scene_stage<NT, NP, PAD>(a, lay, c, fb, cnt, [] {});
     }
     if (live) {
       __builtin_amdgcn_s_setprio(2);
@@ -1388,12 +1484,12 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   // staging barriers, not in every producer's prologue before them (there it
   // was ~600 instructions per wave, issued one wave after the other on a
   // SIMD, and the first staging barrier waited for the last)
-  if (c.nf > 0) scene_stage<64 * (kRecW + NP), NP, NLL>(a, lay, c, 0, c.nf < lay.fc ? c.nf : lay.fc, [] {});
+  if (c.nf > 0) scene_stage<64 * (kRecW + NP), NP, !GRAD, NLL>(a, lay, c, 0, c.nf < lay.fc ? c.nf : lay.fc, [] {});
   for (int fb = 0; fb < c.nf; fb += lay.fc) {
     const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
     if (fb > 0) {
       scene_pos_dma<64 * (kRecW + NP)>(a, lay, c, fb, cnt);
-      scene_stage<64 * (kRecW + NP), NP, NLL>(a, lay, c, fb, cnt, [] {});
+      scene_stage<64 * (kRecW + NP), NP, !GRAD, NLL>(a, lay, c, fb, cnt, [] {});
     }
     if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
     const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
@@ -1436,7 +1532,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       if (CR) __builtin_amdgcn_s_setprio(2);
       else if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(1);   // the first round's heads
       const FrameHeadOut hd =
-          frame_head(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
+          frame_head<!GRAD>(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                      c.sFlag + fl, f + 1,
                      a.A_out && mine ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
                      a.cost_out && mine ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr,
@@ -1757,7 +1853,7 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   };
   if (c.wv < kRecW) {
     scalars();
-    scene_recurrence<TPW, NP, CR>(a, lay, c);
+    scene_recurrence<TPW, NP, CR, !GRAD>(a, lay, c);
     if (GRAD) rec_grad_work<NP, PM, NLL>(a, lay, c);
   } else {
     scalars();
