@@ -334,3 +334,29 @@ def test_coresident_launches_in_flight(gpu, name, S):
         assert torch.equal(p.out.pred, a.pred)
         assert torch.equal(p.out.h, a.h)
         assert torch.equal(p.out.metrics, a.metrics)
+
+
+@pytest.mark.parametrize("coresident", [False, True])
+def test_step_stride2_matches_oracle(gpu, coresident):
+    """Window stride 2 (frame f's window starts at row 2 f): 46 window rows,
+    so the staging has more tasks than a co-resident workgroup has producer
+    waves (4 V / VG tiles, K1 / K2 and the padded operands' constants over 4
+    producers: the task loop wraps), and the frame heads read their window
+    rows at 2 f + k."""
+    S, Nmax, H, F = 3, 32, 128, 20
+    b = make_batch(S, Nmax, H, F=2 * F - 1, seed=5, h0_scale=1.0)   # W = 2 (F - 1) + 8 rows
+    tg = np.ascontiguousarray(b.targets[:, ::2])                    # any F target sets
+    params = fs.init_params(Nmax, seed=0, device=gpu)
+    t = b.to_device(gpu)
+    out = fs.step_fused(params, t["pos"], t["vislet"], t["G"], torch.from_numpy(tg).to(gpu),
+                        t["n_active"], t["h0"], stride=2, coresident=coresident)
+    torch.cuda.synchronize()
+    pred, hh, met = out.pred.cpu().numpy(), out.h.cpu().numpy(), out.metrics.cpu().numpy()
+    w = params.numpy()
+    for s in range(S):
+        pr, h, m, _ = ref.scene_step(b.pos[s], b.vislet[s], b.G[s], w, tg[s], b.n_active[s],
+                                     b.h0[s], n_frames=F, stride=2)
+        n = int(b.n_active[s])
+        assert close(pred[s, :, :, :n].reshape(F, 2, 12, n), pr) <= TOL, s
+        assert close_h(hh[s], h), s
+        assert close(met[s, :6], m[:6]) <= TOL, s
