@@ -40,6 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from multimodaltraj_2_amd import frame_step as fs          # noqa: E402
+from multimodaltraj_2_amd.dist import reap_pending_work     # noqa: E402
 from multimodaltraj_2_amd.synthetic import CONFIGS, FRAMES_PER_SCENE, make_batch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -66,6 +67,84 @@ def algorithmic_bytes(b, H, params_bytes, targets_shared=False):
         + (FT * nact * L2 * 4).sum() + S * D * H * 4 + S * 4 + params_bytes + extra
     wr = (F * L2 * nact * 4).sum() + S * D * H * 4 + S * 8 * 4
     return int(rd + wr)
+
+
+# ---------------------------------------------------------------------------
+# algorithmic flops: the roof a launch is bound by
+# ---------------------------------------------------------------------------
+FP32_PEAK_TFS = 157.3          # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA (16x16x4 f32) peak
+RIDGE = FP32_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)      # 19.7 flop/B
+GRID_LSTM_FLOPS = 16 * (16 // 4) * 126                     # D * (D/4) * 126 = 8,064 per frame
+
+
+def flops_per_frame(n, H, grid_lstm=False):
+    """F_frame = 776 N + 20,000 + 672 H for one (scene,
+    frame) unit of train.py:197-276 with N active pedestrians — embed 2TND +
+    2D^2T, vislet 4ND, E 2T(D+2)D + TD, Rm 4TD, A 2D^2T + TD, Cst 2DT^2, Y
+    48T^2 + 48TN, the attention softmax ~5D^2, the recurrence 2D^2H + 10DH,
+    the errors ~72N (D 16, T 8; transcendentals one flop each; the constant
+    terms sum to 19,968, which the survey rounds to 20,000 and so do we);
+    + 8,064 with the GridLSTM encoder (helper.py:31-39)."""
+    return 776 * n + 20_000 + 672 * H + (GRID_LSTM_FLOPS if grid_lstm else 0)
+
+
+def bwd_flops_per_frame(n, loss="l2"):
+    """The train mode's gradient of one frame (the loss's dependency cone:
+    pred = (Wc (E g)) Wo with E = Wv X + bv, X = [Wii (Bv Wi); vislet Wi];
+    A and the recurrence do not reach pred, train.py:254).  dY 72N (L2: the
+    residual, its square and sum) or ~480N (the bivariate-Gaussian NLL and
+    its gradient, 40 flops per (pedestrian, step)); dWo = M^T dY and dM = dY
+    Wo^T 384N each; dWc = dM Cst^T and dCst = Wc^T dM 3,072 each; dE =
+    dCst g^T 2,048; dWv = dE X^T and dX = Wv^T dE 4,608 each, dbv 128; dWii
+    = dX0 U^T and dU = Wii^T dX0 4,096 each; dWi = Bv^T dU + vislet^T dVe
+    256N + 64N (data, g and G get no gradient)."""
+    return (72 if loss == "l2" else 480) * n + 384 * n * 2 + 256 * n + 64 * n + 25_728
+
+
+def _frames_and_active(b):
+    F = b.n_frames.astype(np.int64) if b.n_frames is not None else np.full(b.S, b.F, np.int64)
+    return F, b.n_active.astype(np.int64)
+
+
+def algorithmic_flops(b, H, grid_lstm=False):
+    """Flops of one g2k_step_fused_f32 launch: every scene's frames at its
+    active pedestrian count."""
+    F, n = _frames_and_active(b)
+    return int((F * flops_per_frame(n, H, grid_lstm)).sum())
+
+
+def train_algorithmic_flops(b, H, P, loss="l2"):
+    """One train step: the forward's flops, the gradient's, the fixed-order
+    sum of the per-scene [P + 2] rows and the RMSProp + clip update (~8 per
+    parameter)."""
+    F, n = _frames_and_active(b)
+    return algorithmic_flops(b, H) + int((F * bwd_flops_per_frame(n, loss)).sum()) \
+        + b.S * (P + 2) + 8 * P
+
+
+def roofline(abytes, aflops, kern_s, step_s):
+    """The contract's roofline object for one kernel: ``bound`` by the
+    launch's arithmetic intensity against the FP32 ridge (157.3 TF/s over 8
+    TB/s = 19.7 flop/B): "hbm" (achieved in GB/s) or "mfma" (the FP32 compute
+    roof — on gfx950 the f32 MFMA and the vector peak are the same 157.3
+    TF/s; achieved in TFLOP/s).  Both fractions are carried for one launch
+    (kern_s) and per step of the timed loop (step_s)."""
+    inten = aflops / abytes
+    f_hbm, f_fl = abytes / kern_s / 1e9 / HBM_PEAK_GBS, aflops / kern_s / 1e12 / FP32_PEAK_TFS
+    p_hbm, p_fl = abytes / step_s / 1e9 / HBM_PEAK_GBS, aflops / step_s / 1e12 / FP32_PEAK_TFS
+    compute = inten >= RIDGE
+    r = {"bound": "mfma" if compute else "hbm",
+         "achieved": aflops / kern_s / 1e12 if compute else abytes / kern_s / 1e9,
+         "peak": FP32_PEAK_TFS if compute else HBM_PEAK_GBS,
+         "unit": "TFLOP/s" if compute else "GB/s"}
+    r["frac"] = r["achieved"] / r["peak"]
+    r.update({"algorithmic_bytes": int(abytes), "flops": int(aflops), "intensity": inten,
+              "ridge": RIDGE, "frac_hbm": f_hbm, "frac_flops": f_fl,
+              "frac_hbm_per_step": p_hbm, "frac_flops_per_step": p_fl,
+              "achieved_per_step": (aflops / step_s / 1e12) if compute else abytes / step_s / 1e9,
+              "bound_note": "mfma = the FP32 compute roof (f32 MFMA = vector peak, 157.3 TF/s)"
+                            if compute else "HBM roof (8 TB/s)"})
+    return r
 
 
 def train_algorithmic_bytes(b, H, params_bytes, P, targets_shared=False):
@@ -259,6 +338,11 @@ class GraphSteps:
         self.n = n
         self.g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
+        if thread_local:
+            # a process group is up: no eager Work may be left for its
+            # watchdog to query while the capture holds the RCCL stream
+            # (multimodaltraj_2_amd/dist.py reap_pending_work)
+            reap_pending_work()
         # thread_local: a capture that holds an RCCL collective (the process
         # group's watchdog thread keeps querying its events meanwhile)
         with torch.cuda.graph(self.g, stream=stream,
@@ -440,10 +524,10 @@ def main(argv=None):
                     help="train mode: the multi-rank step structure (gradient -> RCCL all-reduce "
                          "-> update); auto = when WORLD_SIZE > 1, on = also on one rank (a "
                          "one-rank nccl group: the structure measured on one GPU)")
-    ap.add_argument("--capture-collective", action="store_true",
-                    help="train mode, collective structure: capture the steps, RCCL all-reduce "
-                         "included, in one HIP graph (default: host launches; see DESIGN.md §8 "
-                         "for the process-group watchdog race this works around)")
+    ap.add_argument("--eager-collective", action="store_true",
+                    help="train mode, collective structure: launch gradient -> RCCL all-reduce "
+                         "-> update from the host every step instead of replaying the steps, "
+                         "collective included, from one HIP graph (the default)")
     ap.add_argument("--selftest-launcher", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 
@@ -481,10 +565,10 @@ def main(argv=None):
     dist = None
     if world > 1 or args.collective == "on":
         import torch.distributed as dist
-        if args.capture_collective:
-            # no reuse of ProcessGroupNCCL's cached events across the capture:
-            # its watchdog thread queried a recycled event while a capture
-            # held it (hipErrorCapturedEvent, one run in three)
+        if not args.eager_collective:
+            # no ProcessGroupNCCL event recycled from a captured Work (its last
+            # record inside a capture) into an eager Work the watchdog polls
+            # (the race itself is closed by reap_pending_work)
             os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
         if world == 1:                   # a one-rank group (--collective on)
             for k, v in dict(MASTER_ADDR="127.0.0.1", RANK="0", WORLD_SIZE="1").items():
@@ -552,7 +636,7 @@ def main(argv=None):
     else:
         kern_s = graph_event_time(GraphSteps(lambda i: one[i % len(one)].run(), R, stream,
                                              thread_local=dist is not None), stream)
-    achieved = abytes / kern_s / 1e9
+    aflops = algorithmic_flops(b, H)
 
     train = None
     if not args.no_train:
@@ -594,15 +678,13 @@ def main(argv=None):
                        "streams": len(streams),
                        "launch": "host launch per step" if args.no_graph else
                                  "HIP graph of the timed steps (one replay)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc[0], "traffic_source": pmc[1],
-                         "kernel": "g2k_step_fused_f32 (g2k_scene_kernel)",
-                         "kernel_us": kern_s * 1e6, "algorithmic_bytes": abytes,
-                         # the timed steps' effective rate: launches overlap (streams,
-                         # co-resident workgroups), so bytes per step / wall per step
-                         # exceeds one launch's rate above
-                         "achieved_per_step": abytes / (elapsed / args.steps) / 1e9},
+            # achieved: one launch alone (kern_s); *_per_step: the timed steps'
+            # effective rate (launches overlap on streams / co-resident
+            # workgroups, so it exceeds one launch's rate)
+            "roofline": dict(roofline(abytes, aflops, kern_s, elapsed / args.steps),
+                             traffic=pmc[0], traffic_source=pmc[1],
+                             kernel="g2k_step_fused_f32 (g2k_scene_kernel)",
+                             kernel_us=kern_s * 1e6),
             "cpu_baseline": cpu,
             "ade_fde_all_ranks": {"ADE": float(m[0] / max(m[1], 1)),
                                   "FDE_frob_per_frame": float(np.sqrt(m[2]) / max(m[5], 1))},
@@ -640,19 +722,17 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
     def step(i):
         last["g"] = ts.run(i % K)
 
-    # one rank: one C call per step (gradient + update), replayed from a HIP
-    # graph; across ranks gradient -> RCCL all-reduce -> update on the plans'
-    # stream from host launches, or (--capture-collective) replayed from a HIP
-    # graph with the collective captured beside the kernels (one eager step
-    # first: the communicator and RCCL's own buffers exist before capture;
-    # then a pause so that the process group's watchdog has reaped that
-    # step's work before the capture starts)
-    graph = not args.no_graph and (not coll or args.capture_collective)
+    # one rank: one C call per step (gradient + update); across ranks
+    # gradient -> RCCL all-reduce -> update on the plans' stream.  Both are
+    # replayed from a HIP graph, the collective captured beside the kernels
+    # (one eager step first: the communicator and RCCL's own buffers exist
+    # before capture; GraphSteps then reaps that step's Work from the
+    # process group's watchdog before it captures); --eager-collective
+    # launches the multi-rank steps from the host instead
+    graph = not args.no_graph and not (coll and args.eager_collective)
     in_graph = False
     if graph and coll:
         step(0)
-        torch.cuda.synchronize()
-        time.sleep(0.5)
     if graph:
         el, gm = timed_graph(step, args.steps, args.warmup, dist, torch.cuda.synchronize, stream,
                              thread_local=dist is not None)
@@ -664,7 +744,7 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
     gl = last["g"].double().cpu().numpy()
     parts = collective_parts(ts, stream, K, graph) if coll else None
     abytes = train_algorithmic_bytes(b, H, pbytes, ts.P, layout["targets_shared"])
-    achieved = abytes / kern_s / 1e9
+    aflops = train_algorithmic_flops(b, H, ts.P, args.loss)
     pmc = load_pmc(args.config + "_train")
     return {"metric": f"frames/sec (obs=8,pred=12) g2k_lstm_mcr train step + "
                       f"{'L2' if args.loss == 'l2' else 'bivariate-Gaussian NLL'} loss gradient + "
@@ -678,11 +758,11 @@ def time_train(args, params, batches, dev, dist, S, F, H, world, b, pbytes, K, l
             "collective_parts_us": parts,
             "loss_per_prediction_last_step": float(gl[-2] / max(gl[-1], 1.0)),
             "optimizer": "RMSProp lr 0.005 decay 0.95, global-norm clip 10 (argParser.py:38-47)",
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc[0], "traffic_source": pmc[1],
-                         "kernel": ts.kernel_names, "step_us": kern_s * 1e6,
-                         "algorithmic_bytes": abytes}}
+            # one step alone (the graph's steps back to back: kern_s) and the
+            # timed loop's rate
+            "roofline": dict(roofline(abytes, aflops, kern_s, el / args.steps),
+                             traffic=pmc[0], traffic_source=pmc[1],
+                             kernel=ts.kernel_names, step_us=kern_s * 1e6)}
 
 
 if __name__ == "__main__":

@@ -51,3 +51,30 @@ def allreduce_grad(buf: torch.Tensor, group=None, force: bool = False) -> torch.
     if dist.is_available() and dist.is_initialized() and (force or dist.get_world_size(group) > 1):
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
     return buf
+
+
+def reap_pending_work(group=None) -> None:
+    """Before capturing a collective into a HIP graph: synchronize, then block
+    until the process group's watchdog thread holds no eager Work.
+
+    Why (the r7m abort): ProcessGroupNCCL's watchdog polls every
+    eager Work it holds with ``hipEventQuery`` on the Work's end event, which
+    was recorded on the group's RCCL stream.  A captured collective puts that
+    same RCCL stream into capture mode (it waits on the capturing stream), and
+    HIP answers a query of an event recorded on a stream that is capturing
+    with hipErrorCapturedEvent — the watchdog treats that as fatal (SIGABRT).
+    Captured Works are never handed to the watchdog, so the race exists only
+    for eager Works still listed when a capture starts (the warm-up step, a
+    barrier, a metric all-reduce: reaped ~100 ms after they finish).  This
+    torch build's capture_begin no longer waits for them, so we do:
+    ``ProcessGroup._wait_for_pending_works`` returns once the watchdog's list
+    is empty, and the caller issues no eager collective until the capture
+    ends.  A no-op without a process group or on a backend with no watchdog
+    (gloo)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    pg = group if group is not None else dist.group.WORLD
+    if dist.get_backend(pg) != "nccl":
+        return
+    torch.cuda.synchronize()
+    pg._wait_for_pending_works()

@@ -58,7 +58,8 @@ class EncoderChain:
             raise ValueError("the encoder chain runs on the GPU only (no CPU fallback)")
         S, F = int(pos.shape[0]), int(targets.shape[1])
         D, Nmax = fs.HIDDEN_LEN, int(pos.shape[2])
-        if tuple(h.shape[:2]) != (1, D) or not h.is_contiguous():
+        fs._check_dev("h", h, dev, torch.float32)
+        if h.dim() != 3 or tuple(h.shape[:2]) != (1, D):
             raise ValueError("h must be one contiguous chain [1, D, H]")
         X, Rel = fs.frame_embed(self.params, pos, vislet, n_active, F, stride=stride,
                                 stream=stream)
@@ -79,8 +80,12 @@ class EncoderChain:
         u, fsz = int(c.num_units), int(c.feature_size)
         if tuple(c.W.shape) != (fsz + 2 * u, 3 * u) or tuple(c.b.shape) != (3 * u,):
             raise ValueError(f"cell W must be [{fsz + 2 * u}, {3 * u}] and b [{3 * u}]")
-        if c.peep is not None and tuple(c.peep.shape) != (4, u):
-            raise ValueError(f"cell peep must be [4, {u}]")
+        if c.peep is not None:
+            if tuple(c.peep.shape) != (4, u):
+                raise ValueError(f"cell peep must be [4, {u}]")
+            if c.peep.dtype != torch.float32 or c.peep.device != dev:
+                raise TypeError(f"cell peep: {c.peep.dtype} on {c.peep.device}, expected "
+                                f"torch.float32 on {dev}")
         peep = None if c.peep is None else c.peep.contiguous()
         W, b, Gc = c.W.contiguous(), c.b.contiguous(), G.contiguous()
         lib = _lib.load()

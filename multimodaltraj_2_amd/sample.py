@@ -213,6 +213,7 @@ def save_results(results, save_dir, log=print):
     the current directory without one).  Returns the path."""
     import pickle
     log("Saving results")
+    os.makedirs(save_dir or ".", exist_ok=True)
     path = os.path.join(save_dir or ".", "social_results.pkl")
     with open(path, "wb") as f:
         pickle.dump(results, f)

@@ -220,21 +220,25 @@ class TrainStep:
                  n_frames=None, ped_mask=None, stride=1, lam=LAMBDA, out=None, group=None,
                  pred_layout="band", targets_shared=False, frames=None, loss="l2", split=0,
                  stream=None, collective=None):
-        self._layout = dict(pred_layout=pred_layout, targets_shared=targets_shared, frames=frames,
-                            loss=loss, split=split, stream=stream)
-        self.flat, self.params = flat_params(params, loss)
-        self.P = self.flat.numel()
-        self.ms = torch.ones_like(self.flat) if rmsprop else None
-        self.lr, self.decay, self.grad_clip = lr, decay, grad_clip
         self.group = group
         self.world = (dist.get_world_size(group)
                       if dist.is_available() and dist.is_initialized() else 1)
         # the multi-rank structure (gradient -> all-reduce -> update); True on
         # one rank forces it (a one-rank group still issues the collective)
         self.collective = self.world > 1 if collective is None else bool(collective)
+        if self.world > 1 and not self.collective:
+            # each rank would apply its own shard's gradient: silent drift
+            raise ValueError(f"collective=False in a {self.world}-rank group: the ranks' "
+                             "gradients must be all-reduced (collective=None or True)")
         if self.collective and self.world == 1 and not (dist.is_available()
                                                         and dist.is_initialized()):
             raise ValueError("collective=True needs an initialised process group")
+        self._layout = dict(pred_layout=pred_layout, targets_shared=targets_shared, frames=frames,
+                            loss=loss, split=split, stream=stream)
+        self.flat, self.params = flat_params(params, loss)
+        self.P = self.flat.numel()
+        self.ms = torch.ones_like(self.flat) if rmsprop else None
+        self.lr, self.decay, self.grad_clip = lr, decay, grad_clip
         self._lam, self._stride = lam, stride
         self._slots = []
         self.bind(pos, vislet, G, targets, n_active, h, n_frames=n_frames, ped_mask=ped_mask,

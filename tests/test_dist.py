@@ -141,6 +141,13 @@ def _structure_worker(rank, world, port, S, steps, q):
     from oracle import g2k_ref as ref
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    # collective=False across ranks would let the replicas drift: refused
+    # before anything is bound
+    try:
+        tsm.TrainStep(None, None, None, None, None, None, None, collective=False)
+        refused = False
+    except ValueError:
+        refused = True
     lo, hi = shard_scenes(S, rank, world)
     log = []
     P = _scene_grads(S, 0, 1).numel() - 2
@@ -168,7 +175,7 @@ def _structure_worker(rank, world, port, S, steps, q):
     for _ in range(steps):
         ts._slots[0].grad.copy_(shard)
         ts.run(0)
-    q.put((rank, log, ts.flat.numpy(), ts.ms.numpy()))
+    q.put((rank, log, ts.flat.numpy(), ts.ms.numpy(), refused))
     dist.destroy_process_group()
 
 
@@ -195,7 +202,8 @@ def test_two_rank_gloo_train_step_structure():
     for _ in range(steps):
         flat, ms = ref.optimizer_update(flat, ms, g[:-2], float(g[-1]), 0.005, 0.95, 10.0)
     for r in range(world):
-        log, f, m = got[r]
+        log, f, m, refused = got[r]
+        assert refused, "TrainStep(collective=False) in a 2-rank group must raise"
         assert log == ["gradient", "allreduce", "update"] * steps
         np.testing.assert_allclose(f, flat, rtol=1e-12, atol=1e-14)
         np.testing.assert_allclose(m, ms, rtol=1e-12, atol=1e-14)

@@ -43,6 +43,7 @@ from __future__ import annotations
 
 import ast
 import contextlib
+import hashlib
 import os
 import sys
 import types
@@ -65,7 +66,62 @@ PRED_LEN = 12
 
 # --------------------------------------------------------------------------
 # The reference's statements as callables (ast, at generation time)
+#
+# /root/reference is untrusted text, so nothing of it is executed unless
+#   (1) the exact source lines the statements span hash to the digest pinned
+#       below — the text that was read and reviewed when this tool was written
+#       (a changed reference refuses to run; re-review, then re-pin), and
+#   (2) the extracted AST passes an allow-list: no import, no global/nonlocal,
+#       no dunder attribute, no name that reaches the interpreter, the file
+#       system or the process (open, exec, eval, os, sys, ...).
+# The compiled code runs with a namespace holding only numpy and the builtins
+# the blocks use (print is redirected to /dev/null by ``quiet``).
 # --------------------------------------------------------------------------
+PINNED = {
+    ("sample.py", 21, 82): "d8610e3210886d5b3e7ea1036c022c091b01a0141aac8b23a330486ebf90891c",
+    ("train.py", 636, 662): "2a04e2aa6a8bd8805698c6b7984c04d08fed341a1d7b3aaf92794516a1467b6b",
+    ("train.py", 668, 674): "8bc20d5966bf241ce7cd15811ebf8d91a0fa2a4aa1b301d87959497adad2c901",
+    ("train.py", 254, 276): "bc5446c8686aaf19cb7ee07a5279f9bef5de84ac3b8bb054635dc8feb883508c",
+}
+_DENY = {"open", "exec", "eval", "compile", "__import__", "getattr", "setattr", "delattr",
+         "globals", "locals", "vars", "os", "sys", "subprocess", "input", "breakpoint",
+         "importlib", "builtins", "__builtins__", "memoryview", "type", "object"}
+_BUILTINS = {k: __builtins__[k] if isinstance(__builtins__, dict) else getattr(__builtins__, k)
+             for k in ("print", "len", "range", "zip", "list", "dict", "enumerate", "float", "int",
+                       "abs", "min", "max", "sum", "KeyError", "IndexError", "ValueError",
+                       "TypeError", "ZeroDivisionError", "Exception", "tuple", "round", "iter",
+                       "next", "str", "bool", "sorted", "reversed", "isinstance", "map", "any",
+                       "all", "StopIteration", "RuntimeError", "AttributeError",
+                       "FloatingPointError")}
+
+
+def _pin(fname, lines, src):
+    lo, hi = min(a for a, _ in lines), max(b for _, b in lines)
+    text = "".join(src.splitlines(keepends=True)[lo - 1:hi])
+    digest = hashlib.sha256(text.encode()).hexdigest()
+    want = PINNED.get((fname, lo, hi))
+    if digest != want:
+        raise RuntimeError(f"{fname}:{lo}-{hi}: source digest {digest} is not the pinned "
+                           f"{want}: the reference text changed; review it and re-pin")
+
+
+def _allow(nodes, where):
+    for top in nodes:
+        for n in ast.walk(top):
+            if isinstance(n, (ast.Import, ast.ImportFrom, ast.Global, ast.Nonlocal, ast.Lambda,
+                              ast.ClassDef, ast.AsyncFunctionDef, ast.Await, ast.Yield,
+                              ast.YieldFrom)):
+                raise RuntimeError(f"{where}: {type(n).__name__} at line {n.lineno} not allowed")
+            if isinstance(n, ast.Name) and n.id in _DENY:
+                raise RuntimeError(f"{where}: name {n.id!r} at line {n.lineno} not allowed")
+            if isinstance(n, ast.Attribute) and n.attr.startswith("__"):
+                raise RuntimeError(f"{where}: attribute {n.attr!r} at line {n.lineno} not allowed")
+
+
+def _namespace():
+    return {"np": np, "__builtins__": dict(_BUILTINS)}
+
+
 def _find(body, lo, hi, out):
     for st in body:
         if st.lineno >= lo and st.end_lineno <= hi:
@@ -81,26 +137,36 @@ def _find(body, lo, hi, out):
 def ref_block(fname, lo, hi, params, returns):
     """The statements of /root/reference/<fname> lying wholly in lines lo..hi
     (one contiguous run of one body) as ``f(**params) -> returns``."""
-    tree = ast.parse(open(os.path.join(REF, fname)).read())
+    src = open(os.path.join(REF, fname)).read()
+    tree = ast.parse(src)
     stmts = _find(tree.body, lo, hi, [])
     if not stmts:
         raise RuntimeError(f"{fname}:{lo}-{hi}: no statements")
+    _pin(fname, [(s.lineno, s.end_lineno) for s in stmts], src)
+    _allow(stmts, f"{fname}:{lo}-{hi}")
     ret = ast.Return(value=ast.Tuple(elts=[ast.Name(id=r, ctx=ast.Load()) for r in returns],
                                      ctx=ast.Load()))
     fn = ast.FunctionDef(name="_blk", args=ast.arguments(
         posonlyargs=[], args=[ast.arg(arg=p) for p in params], kwonlyargs=[], kw_defaults=[],
         defaults=[]), body=stmts + [ret], decorator_list=[], returns=None, type_comment=None)
     mod = ast.fix_missing_locations(ast.Module(body=[fn], type_ignores=[]))
-    ns = {"np": np}
+    ns = _namespace()
     exec(compile(mod, f"{REF}/{fname}:{lo}-{hi}", "exec"), ns)
     return ns["_blk"], [(type(s).__name__, s.lineno, s.end_lineno) for s in stmts]
 
 
 def ref_function(fname, name):
-    tree = ast.parse(open(os.path.join(REF, fname)).read())
+    src = open(os.path.join(REF, fname)).read()
+    tree = ast.parse(src)
     fn = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == name]
+    if len(fn) != 1:
+        raise RuntimeError(f"{fname}: {len(fn)} functions named {name}")
+    _pin(fname, [(fn[0].lineno, fn[0].end_lineno)], src)
+    if fn[0].decorator_list or fn[0].args.defaults or fn[0].args.kw_defaults:
+        raise RuntimeError(f"{fname}:{name}: decorators / defaults not allowed")
+    _allow(fn, f"{fname}:{name}")
     mod = ast.fix_missing_locations(ast.Module(body=fn, type_ignores=[]))
-    ns = {"np": np}
+    ns = _namespace()
     exec(compile(mod, f"{REF}/{fname}:{name}", "exec"), ns)
     return ns[name], (fn[0].lineno, fn[0].end_lineno)
 
