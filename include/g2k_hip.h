@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define G2K_ABI_VERSION 8
+#define G2K_ABI_VERSION 9
 
 enum {
   G2K_OK = 0,
@@ -94,10 +94,16 @@ typedef struct g2k_dims {
  * zeroes the scene tickets in it on its own stream first (a memset ahead of
  * the kernel), so no earlier call — an aborted one included — can leave state
  * behind.  One workspace per stream: two launches in flight must not share
- * one.  The automatic choice and the workspace sizes depend on the CU count of
- * the device current when they are queried (hipGetDevice: these planning
- * calls initialise the HIP runtime); a launch re-derives them for the device
- * current at launch time and rejects a workspace smaller than that needs. */
+ * one.  An explicit G2K_STEP_SPLIT(x) makes every size and the launch
+ * independent of any device.  With 0 (automatic), the planning calls
+ * (g2k_step_split, g2k_*_workspace_bytes) answer for the device current when
+ * they are queried (hipGetDevice: they initialise the HIP runtime), while a
+ * LAUNCH resolves the automatic choice for the device of the stream it is
+ * given (hipStreamGetDevice; the null stream: the current device) and rejects
+ * a workspace smaller than that split needs.  Planners that must not depend
+ * on the current device ask g2k_step_split_for_cus(d, cus) — host arithmetic,
+ * no HIP call — with the CU count of the device they will launch on, and pass
+ * the answer as G2K_STEP_SPLIT(x) (ABI 9; what the Python plans do). */
 #define G2K_STEP_SPLIT_SHIFT 8
 #define G2K_STEP_SPLIT_MASK (7 << G2K_STEP_SPLIT_SHIFT)
 #define G2K_STEP_SPLIT(x) ((x) << G2K_STEP_SPLIT_SHIFT)
@@ -127,6 +133,11 @@ int64_t g2k_step_workspace_bytes(const g2k_dims* d);
 /* Workgroups per scene the step / train entry points use for `d` (the
  * G2K_STEP_SPLIT request, or the automatic choice); -1 on invalid dims. */
 int32_t g2k_step_split(const g2k_dims* d);
+/* The automatic split for a device with `cus` compute units (the request when
+ * `d` names one; 1 under G2K_STEP_CORESIDENT): host arithmetic only, no HIP
+ * call, so a plan can be sized for its device with or without a GPU present;
+ * -1 on invalid dims or cus < 1 (ABI 9). */
+int32_t g2k_step_split_for_cus(const g2k_dims* d, int32_t cus);
 /* Zero-fill `workspace_bytes` bytes of a workspace on `stream` (hipMemsetAsync).
  * (ABI 6 and earlier required it before a split workspace's first use; since
  * ABI 7 every launch zeroes its tickets itself and this is optional.) */

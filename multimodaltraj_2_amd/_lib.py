@@ -45,6 +45,7 @@ SYMBOLS = {
     "g2k_step_lds_bytes": (c_i64, [ctypes.POINTER(G2KDims)]),
     "g2k_step_workspace_bytes": (c_i64, [ctypes.POINTER(G2KDims)]),
     "g2k_step_split": (ctypes.c_int32, [ctypes.POINTER(G2KDims)]),
+    "g2k_step_split_for_cus": (ctypes.c_int32, [ctypes.POINTER(G2KDims), ctypes.c_int32]),
     "g2k_workspace_init": (c_int, [c_vp, c_i64, c_vp]),
     "g2k_step_fused_f32": (c_int, [ctypes.POINTER(G2KDims), ctypes.POINTER(G2KWeights),
                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -95,7 +96,7 @@ SYMBOLS = {
                                      c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class G2KLibraryError(RuntimeError):

@@ -40,6 +40,22 @@ int device_cus() {
   return n;
 }
 
+// CUs of the device `st` belongs to (the null stream: the current device);
+// 256 when the runtime cannot say
+int stream_cus(hipStream_t st) {
+  hipDevice_t dev = 0;
+  if (st == nullptr || hipStreamGetDevice(st, &dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return device_cus();
+  }
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  return n;
+}
+
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess)
@@ -106,11 +122,21 @@ int validate_step_inputs(const g2k_dims* d, const g2k_weights* w, const float* p
   return G2K_OK;
 }
 
+// The launch's dims with the split made explicit: an automatic request is
+// resolved for the device of the stream the launch goes to (not the current
+// device: a plan may be launched on a stream of another device), so every
+// later scene_split(a.d) — the workspace check, the kernel layout, the row
+// count — agrees with the launch, and a workspace sized for another split is
+// rejected by size.
 StepArgs step_args(const g2k_dims* d, const g2k_weights* w, const float* pos, const float* vislet,
                    const float* G, const float* targets, const int32_t* n_active,
-                   const int32_t* n_frames, const uint8_t* ped_mask, float lambda) {
+                   const int32_t* n_frames, const uint8_t* ped_mask, float lambda,
+                   hipStream_t st) {
   StepArgs a = {};
-  a.d = *d; a.w = *w; a.pos = pos; a.vislet = vislet; a.G = G; a.targets = targets;
+  a.d = *d;
+  if (split_automatic(a.d))
+    a.d.flags |= G2K_STEP_SPLIT(scene_split_cus(a.d, stream_cus(st)));
+  a.w = *w; a.pos = pos; a.vislet = vislet; a.G = G; a.targets = targets;
   a.n_active = n_active; a.n_frames = n_frames; a.ped_mask = ped_mask; a.lambda = lambda;
   return a;
 }
@@ -132,8 +158,8 @@ int train_launch(StepArgs a, float* grad, void* workspace, int64_t workspace_byt
   if (loss_nll(a.d) && !a.w.head) return set_err(G2K_EINVAL, "G2K_STEP_LOSS_NLL needs weights->head");
   const int64_t need = grad_rows_bytes(&a.d);
   if (!workspace || workspace_bytes < need)
-    return set_err(G2K_EINVAL, "workspace of %lld bytes needed (got %lld)", (long long)need,
-                   (long long)workspace_bytes);
+    return set_err(G2K_EINVAL, "workspace of %lld bytes needed for %d workgroups per scene (got %lld)",
+                   (long long)need, scene_split(a.d), (long long)workspace_bytes);
   int rc;
   if (a.d.S == 0 || a.d.F == 0) {
     if (hipMemsetAsync(grad, 0, (size_t)width * 4, st) != hipSuccess)
@@ -181,6 +207,12 @@ int32_t g2k_step_split(const g2k_dims* d) {
   return scene_split(*d);
 }
 
+int32_t g2k_step_split_for_cus(const g2k_dims* d, int32_t cus) {
+  if (validate_common(d, true, false, kTrainFlags | kStepFlags) != G2K_OK) return -1;
+  if (cus < 1) { set_err(G2K_EINVAL, "cus=%d < 1", cus); return -1; }
+  return scene_split_cus(*d, cus);
+}
+
 int64_t g2k_step_workspace_bytes(const g2k_dims* d) {
   if (validate_common(d, true, false, kStepFlags) != G2K_OK) return -1;
   return split_ws_bytes(*d);   // one workgroup per scene: every intermediate stays on chip
@@ -210,11 +242,12 @@ int g2k_step_fused_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
     return set_err(G2K_EINVAL, "h_in and h_out must be 16-byte aligned");
   if (workspace_bytes < 0) return set_err(G2K_EINVAL, "negative workspace size");
   if (d->S == 0) return G2K_OK;
-  const int64_t need = split_ws_bytes(*d);
+  StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda,
+                         (hipStream_t)stream);
+  const int64_t need = split_ws_bytes(a.d);
   if (need > 0 && (!workspace || workspace_bytes < need))
-    return set_err(G2K_EINVAL, "workspace of %lld bytes needed (got %lld)", (long long)need,
-                   (long long)workspace_bytes);
-  StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda);
+    return set_err(G2K_EINVAL, "workspace of %lld bytes needed for %d workgroups per scene (got %lld)",
+                   (long long)need, scene_split(a.d), (long long)workspace_bytes);
   a.h_in = h_in; a.h_out = h_out; a.pred = pred; a.metrics = metrics; a.A_out = A_out;
   a.cost_out = cost_out;
   split_ws_bind(a, workspace);
@@ -240,7 +273,8 @@ int g2k_train_step_f32(const g2k_dims* d, const g2k_weights* w, const float* pos
     return set_err(G2K_EINVAL, "a required buffer pointer is NULL");
   if (!aligned16(h_in) || !aligned16(h_out))
     return set_err(G2K_EINVAL, "h_in and h_out must be 16-byte aligned");
-  StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda);
+  StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda,
+                         (hipStream_t)stream);
   a.h_in = h_in; a.h_out = h_out; a.pred = pred; a.metrics = metrics;
   return train_launch(a, grad, workspace, workspace_bytes, params, ms, lr, decay, grad_clip,
                       (hipStream_t)stream);
@@ -385,7 +419,8 @@ int g2k_step_grad_f32(const g2k_dims* d, const g2k_weights* w, const float* pos,
                       void* stream) {
   int rc = validate_step_inputs(d, w, pos, vislet, G, targets, n_active, true);
   if (rc) return rc;
-  StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda);
+  StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda,
+                         (hipStream_t)stream);
   return train_launch(a, grad, workspace, workspace_bytes, nullptr, nullptr, 0.f, 0.f, 0.f,
                       (hipStream_t)stream);
 }
@@ -399,7 +434,8 @@ int g2k_step_grad_update_f32(const g2k_dims* d, const g2k_weights* w, const floa
   if (!params) return set_err(G2K_EINVAL, "params is NULL");
   int rc = validate_step_inputs(d, w, pos, vislet, G, targets, n_active, true);
   if (rc) return rc;
-  StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda);
+  StepArgs a = step_args(d, w, pos, vislet, G, targets, n_active, n_frames, ped_mask, lambda,
+                         (hipStream_t)stream);
   return train_launch(a, grad, workspace, workspace_bytes, params, ms, lr, decay, grad_clip,
                       (hipStream_t)stream);
 }

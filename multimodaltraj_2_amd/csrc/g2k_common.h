@@ -412,20 +412,27 @@ struct StepArgs {
 };
 
 // Workgroups per scene of the fused step (G2K_STEP_SPLIT, include/g2k_hip.h):
-// the requested count, else enough to cover the current device's CUs (4 at
-// most), never more than the frames to share.
+// the requested count, else enough to cover `cus` CUs (4 at most), never more
+// than the frames to share.  Host arithmetic only: no HIP call.
 constexpr int kMaxSplit = 4;
 int device_cus();   // CUs of the current device (g2k_abi.hip; 256 without a device)
-inline int scene_split(const g2k_dims& d) {
+inline bool split_automatic(const g2k_dims& d) {
+  return ((d.flags & G2K_STEP_SPLIT_MASK) >> G2K_STEP_SPLIT_SHIFT) == 0 &&
+         !(d.flags & G2K_STEP_CORESIDENT);
+}
+inline int scene_split_cus(const g2k_dims& d, int cus) {
   int x = (d.flags & G2K_STEP_SPLIT_MASK) >> G2K_STEP_SPLIT_SHIFT;
   if (x == 0 && (d.flags & G2K_STEP_CORESIDENT)) x = 1;   // launches in flight fill the CUs
-  if (x == 0) {
-    const int cus = device_cus();
-    x = d.S >= cus ? 1 : (d.S > 0 ? cus / d.S : 1);
-  }
+  if (x == 0) x = d.S >= cus ? 1 : (d.S > 0 ? cus / d.S : 1);
   if (x > kMaxSplit) x = kMaxSplit;
   if (x > d.F) x = d.F;
   return x < 1 ? 1 : x;
+}
+// the split of `d`: explicit in the flags (every launch: step_args resolves
+// an automatic request for the stream's device), or — the planning calls
+// without a stream — the automatic choice for the CURRENT device
+inline int scene_split(const g2k_dims& d) {
+  return scene_split_cus(d, split_automatic(d) ? device_cus() : 1);
 }
 // split workspace: the scene tickets (one 64-byte line per 16 scenes), then the partials
 inline int64_t split_ws_bytes(const g2k_dims& d) {

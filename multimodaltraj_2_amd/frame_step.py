@@ -160,16 +160,40 @@ def step_coresidency(S, F, H, Nmax, W, stride, coresident=False) -> int:
     return 2 if step_lds_bytes(S, F, H, Nmax, W, stride, True) <= CORESIDENT_LDS else 1
 
 
-def step_split(S, F, H, Nmax, W, stride, split=0, coresident=False) -> int:
-    """Workgroups per scene the library uses (g2k_step_split: the request, or
-    the automatic choice from the current device's CU count)."""
+def device_cus(device) -> int:
+    """Compute units of the device a plan will launch on."""
+    return int(torch.cuda.get_device_properties(device).multi_processor_count)
+
+
+def split_for_cus(S, F, split=0, coresident=False, cus=256) -> int:
+    """Workgroups per scene for a device with ``cus`` CUs: the request, or the
+    library's automatic choice (g2k_step_split_for_cus, ABI 9: host
+    arithmetic, no HIP call — the same answer with or without a GPU)."""
     lib = _lib.load()
-    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride,
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 128, 1, max(F, 1) + OBS_LEN, 1,
                      step_flags(split=split, coresident=coresident))
-    x = int(lib.g2k_step_split(ctypes.byref(d)))
+    x = int(lib.g2k_step_split_for_cus(ctypes.byref(d), int(cus)))
     if x < 1:
-        _lib.check("g2k_step_split", -1)
+        _lib.check("g2k_step_split_for_cus", -1)
     return x
+
+
+def plan_split(S, F, split, coresident, device) -> int:
+    """The explicit split a plan launches with: an automatic request (0) is
+    resolved HERE for the plan's own device and passed to the library as
+    G2K_STEP_SPLIT(x), so sizing and launch never depend on which device is
+    current (include/g2k_hip.h); 0 stays 0 under G2K_STEP_CORESIDENT (the
+    library's 1)."""
+    if split or coresident:
+        return split
+    return split_for_cus(S, F, 0, False, device_cus(device))
+
+
+def step_split(S, F, H, Nmax, W, stride, split=0, coresident=False, device=None) -> int:
+    """Workgroups per scene a plan on ``device`` (default: the current one)
+    uses: the request, or the automatic choice for that device's CUs."""
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    return split_for_cus(S, F, split, coresident, device_cus(dev))
 
 
 def step_workspace_bytes(S, F, H, Nmax, W, stride) -> int:
@@ -250,8 +274,9 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
     S, W, Nmax, two = pos.shape
     if two != 2:
         raise ValueError(f"pos: last dim {two}, expected 2")
-    flags = step_flags(pred_layout, targets_shared, split=split, coresident=coresident)
     F = step_frames(targets, targets_shared, frames)
+    split = plan_split(S, F, split, coresident, dev)
+    flags = step_flags(pred_layout, targets_shared, split=split, coresident=coresident)
     H = int(h.shape[2])
     params.check(dev)
     if params.nmax != Nmax:

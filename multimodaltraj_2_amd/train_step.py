@@ -25,7 +25,7 @@ import torch.distributed as dist
 from . import _lib
 from .dist import allreduce_grad
 from .frame_step import (HIDDEN_LEN, LAMBDA, OBS_LEN, PRED_LEN, G2KParams, StepPlan, _check_dev,
-                         _ptr, _stream, step_flags, step_frames, workspace)
+                         _ptr, _stream, plan_split, step_flags, step_frames, workspace)
 
 GRAD_ORDER = ("Wi", "Wii", "Wv", "bv", "Wr", "Wc", "Wo")   # g2k_weights order
 NLL_HEAD = 3 * PRED_LEN          # loss "nll": the head [3, L] follows Wo in the flat vector
@@ -91,6 +91,7 @@ class GradPlan:
             _check_dev("ped_mask", ped_mask, dev, torch.uint8)
         if loss == "nll" and params.head is None:
             raise ValueError('loss "nll" needs params.head [3, 12]')
+        split = plan_split(S, F, split, False, dev)       # explicit: device-independent sizes
         d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 64, Nmax, W, stride,
                          step_flags("band", targets_shared, loss, split))
         P = int(lib.g2k_grad_size(ctypes.byref(d)))
@@ -159,6 +160,9 @@ class TrainPlan:
         lib = _lib.load()
         if loss == "nll" and params.head is None:
             raise ValueError('loss "nll" needs params.head [3, 12]')
+        # one explicit split for the forward plan and the train launch alike
+        split = plan_split(int(pos.shape[0]), step_frames(targets, targets_shared, frames), split,
+                           False, pos.device)
         self.fwd = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
                             ped_mask=ped_mask, stride=stride, lam=lam, out=out, stream=stream,
                             pred_layout=pred_layout, targets_shared=targets_shared, frames=frames,

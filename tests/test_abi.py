@@ -201,3 +201,34 @@ def test_encoder_chain_validates():
     assert call(_dims(), nf=None) == -1
     assert call(_dims(), h=ctypes.c_void_p(20)) == -1     # h 16-byte aligned
     assert lib.g2k_last_error()
+
+
+def test_split_sizing_without_a_gpu_is_explicit():
+    """ABI 9: the automatic split for a given CU count is host arithmetic
+    (g2k_step_split_for_cus, no HIP call), and an explicit split makes the
+    workspace size independent of any device (include/g2k_hip.h)."""
+    import ctypes
+
+    from multimodaltraj_2_amd import frame_step as fs
+    lib = _lib.load()
+    assert fs.split_for_cus(256, 20, cus=256) == 1
+    assert fs.split_for_cus(128, 20, cus=256) == 2
+    assert fs.split_for_cus(128, 20, cus=304) == 2
+    assert fs.split_for_cus(64, 20, cus=256) == 4
+    assert fs.split_for_cus(16, 20, cus=256) == 4          # at most kMaxSplit
+    assert fs.split_for_cus(16, 3, cus=256) == 3           # at most F
+    assert fs.split_for_cus(100, 20, cus=80) == 1
+    assert fs.split_for_cus(128, 20, split=3, cus=256) == 3          # the request
+    assert fs.split_for_cus(128, 20, coresident=True, cus=256) == 1  # launches in flight
+    d = _lib.G2KDims(128, 20, 8, 12, 16, 128, 32, 27, 1, 0)
+    assert lib.g2k_step_split_for_cus(ctypes.byref(d), 0) == -1
+    sizes = set()
+    for x in (1, 2, 4):
+        d = _lib.G2KDims(128, 20, 8, 12, 16, 128, 32, 27, 1, fs.step_flags(split=x))
+        nb = lib.g2k_step_workspace_bytes(ctypes.byref(d))
+        assert nb == (0 if x == 1 else (128 + 15) // 16 * 64 + 128 * x * 8 * 4)
+        sizes.add(nb)
+        tb = lib.g2k_train_workspace_bytes(ctypes.byref(d))
+        P = lib.g2k_grad_size(ctypes.byref(d))
+        assert tb == 128 * x * (P + 2) * 4 + 64 + nb       # one gradient row per workgroup
+    assert len(sizes) == 3
