@@ -67,11 +67,27 @@ def _compile(src, verbose):
     return obj
 
 
+def _obj_current(src) -> bool:
+    """The object of `src` is newer than it, every header and this file (a
+    header change rebuilds every translation unit)."""
+    obj = os.path.join(OBJ, os.path.splitext(os.path.basename(src))[0] + ".o")
+    if not os.path.exists(obj):
+        return False
+    t = os.path.getmtime(obj)
+    return all(os.path.getmtime(p) <= t for p in [src] + HDR + [os.path.abspath(__file__)])
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     if force or needs_build():
         os.makedirs(OBJ, exist_ok=True)
-        with ThreadPoolExecutor(max_workers=min(8, len(SRC))) as ex:
-            objs = list(ex.map(lambda s: _compile(s, verbose), SRC + CXX_SRC))
+        units = SRC + CXX_SRC
+
+        def unit(s):
+            if not force and _obj_current(s):
+                return os.path.join(OBJ, os.path.splitext(os.path.basename(s))[0] + ".o")
+            return _compile(s, verbose)
+        with ThreadPoolExecutor(max_workers=min(8, len(units))) as ex:
+            objs = list(ex.map(unit, units))
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

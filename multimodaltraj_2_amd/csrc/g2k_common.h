@@ -128,6 +128,18 @@ __device__ __forceinline__ float sum_rows4(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Partner lane's value across lane groups (q ^ 1 by permlane16, q ^ 2 by
+// permlane32): of the pair a swap returns, one element is this lane's own
+// value, the other the partner's.
+__device__ __forceinline__ float partner16(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return a[0] == __float_as_uint(v) ? __uint_as_float(a[1]) : __uint_as_float(a[0]);
+}
+__device__ __forceinline__ float partner32(float v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return a[0] == __float_as_uint(v) ? __uint_as_float(a[1]) : __uint_as_float(a[0]);
+}
+
 // Sum over all 64 lanes (DPP + permlane, no LDS); every lane gets the result.
 __device__ __forceinline__ float wave_sum(float v) { return sum_rows4(row16_sum(v)); }
 
@@ -187,47 +199,6 @@ __device__ __forceinline__ void error_terms(const float* y, const float* tgt, fl
   acc[3] += l2 * (1.0f / 12.0f);
   acc[4] += sqrtf(fsq);
 }
-
-// ---------------------------------------------------------------------------
-// As = softmax(exp(A) / cumsum(exp(A), axis=0), axis=-1)   (train.py:240)
-// Column pass with a running max so exp never overflows (the ratio
-// exp(a_r) / sum_{k<=r} exp(a_k) is scale-invariant), then a row softmax of
-// values in (0, 1].  `A` is one [16, 16] tile in LDS, transformed in place.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void attn_column_pass(float* A, int c) {
-  float m = -INFINITY, s = 0.f;
-#pragma unroll
-  for (int r = 0; r < kD; ++r) {
-    const float a = A[r * kD + c];
-    const float mn = fmaxf(m, a);
-    const float ea = __expf(a - mn);
-    s = fmaf(s, __expf(m - mn), ea);
-    m = mn;
-    A[r * kD + c] = ea * rcp(s);
-  }
-}
-
-__device__ __forceinline__ void attn_row_pass(float* A, int r, float* gout) {
-  float4* row = reinterpret_cast<float4*>(A + r * kD);
-  float e[kD];
-  float z = 0.f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float4 v = row[k];
-    e[4 * k + 0] = __expf(v.x); e[4 * k + 1] = __expf(v.y);
-    e[4 * k + 2] = __expf(v.z); e[4 * k + 3] = __expf(v.w);
-  }
-#pragma unroll
-  for (int k = 0; k < kD; ++k) z += e[k];
-  const float rz = rcp(z);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float4 v = make_float4(e[4 * k] * rz, e[4 * k + 1] * rz, e[4 * k + 2] * rz, e[4 * k + 3] * rz);
-    row[k] = v;
-    if (gout) reinterpret_cast<float4*>(gout + r * kD)[k] = v;
-  }
-}
-
 
 // ---------------------------------------------------------------------------
 // LDS polling for the wave-specialised scene kernel.  The loads are inline

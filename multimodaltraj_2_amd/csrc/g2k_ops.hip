@@ -22,34 +22,82 @@ namespace {
 constexpr int kRecurChunk = 32;   // As tiles resident in LDS
 
 // As = softmax(exp(A) / cumsum(exp(A), axis=0), axis=-1) (train.py:240) of
-// one [16, 16] LDS tile whose first D rows / columns are real: column pass
-// (running max, so exp never overflows: the ratio exp(a_r) / sum_{k<=r}
-// exp(a_k) is shift-invariant) over rows < D, then row softmax over columns
-// < D; padded rows and columns end as exact zeros.
-__device__ __forceinline__ void attn_col(float* A, int c, int D) {
-  float m = -INFINITY, s = 0.f;
-  for (int r = 0; r < kD; ++r) {
-    if (r >= D || c >= D) { A[r * kD + c] = 0.f; continue; }
-    const float a = A[r * kD + c];
-    const float mn = fmaxf(m, a);
-    const float ea = __expf(a - mn);
-    s = fmaf(s, __expf(m - mn), ea);
-    m = mn;
-    A[r * kD + c] = ea * rcp(s);
-  }
-}
-
-__device__ __forceinline__ void attn_row(float* A, int r, int D) {
-  float e[kD];
-  float z = 0.f;
+// one [16, 16] LDS tile whose first D rows / columns are real, by ONE wave,
+// in place: lane (L, q) holds column L, rows 4q .. 4q + 3.  Column pass: the
+// ratio exp(A_r) / sum_{k<=r} exp(A_k) is shift-invariant, so with the
+// column max M, e = exp(A - M) lies in (0, 1] and the prefix sums (in-lane,
+// then across the lane groups by permlane swaps) cannot overflow; a column
+// whose prefix sum underflows (its leading rows ~87 below its max) is redone
+// with running (max, sum) pairs, exact for any finite A.  Then a 16-lane row
+// softmax of values in (0, 1] (DPP).  Padded rows and columns end as exact
+// zeros.  (The fused scene kernel's attn_weights in this kernel family's
+// layout; a serial per-column walk of the 16 rows took ~2.2k cycles on the
+// --use_grid_lstm chain, this ~0.5k.)
+__device__ __forceinline__ void attn_tile_wave(float* A, int D, int lane) {
+  const int L = lane & 15, q = lane >> 4;
+  float aA[4];
+  bool ok[4];
 #pragma unroll
-  for (int k = 0; k < kD; ++k) {
-    e[k] = (r < D && k < D) ? __expf(A[r * kD + k]) : 0.f;
-    z += e[k];
+  for (int i = 0; i < 4; ++i) {
+    aA[i] = A[(4 * q + i) * kD + L];
+    ok[i] = L < D && 4 * q + i < D;
   }
-  const float rz = r < D ? rcp(z) : 0.f;
+  float mx = -INFINITY;
 #pragma unroll
-  for (int k = 0; k < kD; ++k) A[r * kD + k] = e[k] * rz;
+  for (int i = 0; i < 4; ++i) mx = fmaxf(mx, ok[i] ? aA[i] : -INFINITY);
+  mx = fmaxf(mx, partner16(mx));
+  mx = fmaxf(mx, partner32(mx));
+  float e[4], p[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = ok[i] ? __expf(aA[i] - mx) : 0.f;
+  p[0] = e[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) p[i] = p[i - 1] + e[i];
+  const float t1 = partner16(p[3]), t2 = partner32(p[3]), t3 = partner32(t1);
+  const float pre = ((q & 2) ? t2 + t3 : 0.f) + ((q & 1) ? t1 : 0.f);   // groups before q
+  float R[4];
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float P = pre + p[i];
+    bad |= ok[i] && !(P >= 1e-30f);
+    R[i] = e[i] * rcp(P);
+  }
+  if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+    // running (max, sum exp) down the rows; exclusive prefix over the groups
+    // (rows >= D only follow the real ones: they reach no real row's prefix)
+    float m_i[4], s_i[4];
+    float m = aA[0], sacc = 1.0f;
+    m_i[0] = m; s_i[0] = sacc;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      lse_combine(m, sacc, aA[i], 1.0f);
+      m_i[i] = m; s_i[i] = sacc;
+    }
+    const float m1 = partner16(m), s1 = partner16(sacc);
+    const float m2 = partner32(m), s2 = partner32(sacc);
+    const float m3 = partner32(m1), s3 = partner32(s1);
+    float pm = m2, ps = s2;
+    lse_combine(pm, ps, m3, s3);
+    float mp = -INFINITY, sp = 0.f;
+    if (q & 2) { mp = pm; sp = ps; }
+    if (q & 1) {
+      if (q & 2) lse_combine(mp, sp, m1, s1);
+      else { mp = m1; sp = s1; }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float mr = m_i[i], sr = s_i[i];
+      if (q > 0) lse_combine(mr, sr, mp, sp);
+      R[i] = __expf(aA[i] - mr) * rcp(sr);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float ex = ok[i] ? __expf(R[i]) : 0.f;
+    const float z = row16_sum(ex);
+    A[(4 * q + i) * kD + L] = ok[i] ? ex * rcp(z) : 0.f;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -87,9 +135,7 @@ __device__ __forceinline__ void recur_scene(const float* __restrict__ att, float
         }
       }
       __syncthreads();
-      for (int task = tid; task < cnt * kD; task += kRT) attn_col(sAs + (task >> 4) * kD * kD, task & 15, D);
-      __syncthreads();
-      for (int task = tid; task < cnt * kD; task += kRT) attn_row(sAs + (task >> 4) * kD * kD, task & 15, D);
+      for (int fl = wv; fl < cnt; fl += NW) attn_tile_wave(sAs + fl * kD * kD, D, lane);
       __syncthreads();
       for (int fl = 0; fl < cnt; ++fl) {
         const float4 b = *reinterpret_cast<const float4*>(sAs + fl * kD * kD + j * kD + 4 * q);
@@ -373,7 +419,44 @@ struct GridArgs {
   int K;
 };
 
-__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// The cell's nonlinearities, branch-free and short (the --use_grid_lstm
+// chain has two of them per frequency block on its critical path): sigmoid
+// by v_exp + v_rcp (1 ulp); tanh as |x| + |x|^3 p(x^2) below 0.625 (the
+// minimax odd polynomial the device library uses there) and 1 - 2 / (e^{2|x|}
+// + 1) above, both formed and one selected (the library branches on |x| and
+// a wave runs both paths).  |error| <= ~2e-7 against float64 (a6's
+// restatement tolerance is 1e-4, tests/test_gridlstm.py).
+__device__ __forceinline__ float sigmoid_f(float x) { return rcp(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanh_f(float x) {
+  const float ax = fabsf(x), x2 = x * x;
+  float p = fmaf(__int_as_float(0xbbbac73d), x2, __int_as_float(0x3ca908c9));
+  p = fmaf(p, x2, __int_as_float(0xbd5c1c4e));
+  p = fmaf(p, x2, __int_as_float(0x3e088382));
+  p = fmaf(p, x2, __int_as_float(0xbeaaaa99));
+  const float small = fmaf(x2, ax * p, ax);
+  const float t = __builtin_amdgcn_exp2f(ax * (2.f * kLog2e));   // e^{2|x|} (inf: large = 1)
+  const float large = fmaf(rcp(t + 1.f), -2.f, 1.f);
+  return copysignf(ax < 0.625f ? small : large, x);
+}
+
+// One unit's gates from its three gate sums (coupled input / forget gates,
+// peepholes p = (wIf, wIt, wOf, wOt), zero without them: the added terms
+// are then exact zeros).  Written with explicit roundings (__fadd_rn /
+// __fmul_rn are never contracted), so gridlstm_row and the chain's
+// chain_cell produce the same bits whatever their surrounding code lets the
+// compiler fuse.
+struct CellGates {
+  float cfn, ctn, mfn, mtn;
+};
+__device__ __forceinline__ CellGates cell_gates(float zi, float zj, float zo, float cf, float ct,
+                                                const float (&p)[4]) {
+  const float ig = sigmoid_f(__fadd_rn(zi, fmaf(p[0], cf, __fmul_rn(p[1], ct))));
+  const float gg = tanh_f(zj);
+  const float fg = __fsub_rn(1.f, ig), ing = __fmul_rn(ig, gg);
+  const float cfn = fmaf(fg, cf, ing), ctn = fmaf(fg, ct, ing);
+  const float og = sigmoid_f(__fadd_rn(zo, fmaf(p[2], cfn, __fmul_rn(p[3], ctn))));
+  return CellGates{cfn, ctn, __fmul_rn(og, tanh_f(cfn)), __fmul_rn(og, tanh_f(ctn))};
+}
 
 template <int U, int FS>
 __device__ __forceinline__ void gridlstm_row(const GridArgs& a, int64_t r) {
@@ -406,16 +489,11 @@ __device__ __forceinline__ void gridlstm_row(const GridArgs& a, int64_t r) {
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      float gi = z[j];
-      if (peep) gi += a.peep[j] * cf[j] + a.peep[U + j] * ct[j];
-      const float ig = sigmoid_f(gi);                                    // coupled: f = 1 - i
-      const float gg = tanhf(z[U + j]);
-      const float cfn = (1.f - ig) * cf[j] + ig * gg;
-      const float ctn = (1.f - ig) * ct[j] + ig * gg;
-      float go = z[2 * U + j];
-      if (peep) go += a.peep[2 * U + j] * cfn + a.peep[3 * U + j] * ctn;
-      const float og = sigmoid_f(go);
-      const float mfn = og * tanhf(cfn), mtn = og * tanhf(ctn);
+      float pj[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) pj[m] = peep ? a.peep[m * U + j] : 0.f;
+      const CellGates gt = cell_gates(z[j], z[U + j], z[2 * U + j], cf[j], ct[j], pj);
+      const float cfn = gt.cfn, ctn = gt.ctn, mfn = gt.mfn, mtn = gt.mtn;
       srow[2 * U * k + j] = ctn;
       srow[2 * U * k + U + j] = mtn;
       orow[2 * U * k + j] = mtn;
@@ -437,55 +515,256 @@ __global__ void __launch_bounds__(256) g2k_gridlstm_kernel(GridArgs a) {
 // --use_grid_lstm's encoder chain (train.py:197-252 with the encoder stage of
 // :201-207; multimodaltraj_2_amd/encoder_step.py): ONE workgroup walks the
 // frames of S batches in order, per frame the three bodies above — the
-// GridLSTM cell on X[s][f][:D] with h[:, :2uK] as its state (16 lanes, one
-// row each) into Xe, the one-feed forward (attn, cost, pred) from Xe, one
-// recurrence frame on h — separated by workgroup barriers.  The same
-// arithmetic as the three launches per frame (bit-identical), without a
-// launch per body: the chain is latency-bound (one scene's worth of work per
-// frame), so the launches were the cost.  (All global hand-offs stay inside
-// the workgroup: its barriers order them; the CU's vector L1 is shared.)
+// GridLSTM cell on X[s][f][:D] with h[:, :2uK] as its state into Xe, the
+// one-feed forward (attn, cost, pred) from Xe, one recurrence frame on h.
+// The same arithmetic as the three launches per frame (bit-identical: every
+// value is formed by the same operations in the same order), with every
+// hand-off of the chain in LDS: h lives in LDS for the whole launch (read
+// from / written to HBM once), the weights are staged once, a batch's G and
+// Rm once per batch, the next frame's X is fetched into registers at the top
+// of a frame and parked in LDS under its middle, and the outputs (Xe rows,
+// the cell state, attn, cost, pred) are stores nothing waits for.  The cell
+// runs one lane per (row, unit) — 16 U lanes, the units of a row exchanging
+// their m_freq by lane permutes between frequency blocks — and a frame's
+// pred (M @ Wo, which the chain never reads) is formed by waves 1..3 under
+// the next frame's cell.  Per frame: six workgroup barriers (the row-max and
+// numerator exchanges of the recurrence, the feed's three dependent stages,
+// the h hand-off), no HBM round trip.
 // ---------------------------------------------------------------------------
 struct ChainArgs {
-  FwdArgs f;          // d (S = F = 1 per feed), weights, lambda
-  GridArgs g;         // W, b, peep, state = h, state_out (scratch), rows = D, K
+  FwdArgs f;          // d (Nmax), weights, lambda
+  GridArgs g;         // W, b, peep, state_out (the cell state, written per frame)
   const float *X, *Rel, *G;
   const int32_t *n_active, *n_frames;
   float *Xe, *attn, *cost, *pred, *h;
   int S, F, H;
 };
 
-template <int TPW, int U, int FS>
-__global__ void __launch_bounds__(kNT) g2k_encoder_chain_kernel(ChainArgs a) {
-  __shared__ FwdLds lf;
-  __shared__ __attribute__((aligned(16))) float sAs[kD * kD];
-  __shared__ __attribute__((aligned(16))) float sRed[4 * 16 * 4];
-  const int Nmax = a.f.d.Nmax;
-  const size_t xrow = (size_t)(kD + 2) * kD;
-  for (int s = 0; s < a.S; ++s) {
-    const int nf = clampi(a.n_frames[s], 0, a.F);
-    for (int f = 0; f < nf; ++f) {
-      const size_t sf = (size_t)s * a.F + f;
-      if (threadIdx.x < kD) {                                     // train.py:201-207
-        GridArgs g = a.g;
-        g.in = a.X + sf * xrow;
-        g.out = a.Xe + sf * xrow;
-        gridlstm_row<U, FS>(g, threadIdx.x);
-      }
-      __syncthreads();
-      FwdArgs w = a.f;                                            // g2k_lstm_mcr.py:99-124
-      w.X = a.Xe + sf * xrow;
-      w.Rel = a.Rel + (size_t)s * 2 * kD;
-      w.G = a.G + (size_t)s * kD * kT;
-      w.n_active = a.n_active + s;
-      w.A_out = a.attn + sf * kD * kD;
-      w.cost_out = a.cost + sf * kT * kT;
-      w.pred = a.pred + sf * kL2 * Nmax;
-      mcr_feed(w, 0, lf);
-      __syncthreads();
-      recur_scene<TPW, 4>(a.attn + sf * kD * kD, a.h, 0, 1, kD, a.H, sAs, sRed);   // :240-252
-      __syncthreads();
+// m_freq of unit u of this lane's row: the row's U lanes are adjacent in one
+// DPP quad (lane = r U + j), so a quad_perm broadcasts it — no LDS round trip
+// between frequency blocks
+template <int U, int u>
+__device__ __forceinline__ float unit_bcast(float v) {
+  if constexpr (U == 1) return v;
+  else if constexpr (U == 2) return dpp<(u | u << 2 | (2 + u) << 4 | (2 + u) << 6)>(v);
+  else return dpp<u * 0x55>(v);
+}
+template <int U, int u = 0>
+__device__ __forceinline__ void units_bcast(float (&mf)[U], float v) {
+  if constexpr (u < U) {
+    mf[u] = unit_bcast<U, u>(v);
+    units_bcast<U, u + 1>(mf, v);
+  }
+}
+
+// One lane of the cell (row r, unit j): gridlstm_row's arithmetic for the
+// unit's three gate columns.  cw[m][i] = W[i][m U + j], cb[m] = b[m U + j],
+// cp[m] = peep[m U + j] (zero without peepholes, as gridlstm_row).  The dot
+// products' terms over x_k and m_time (everything but m_freq, which comes
+// last in their order) are formed for every block up front, so a block's
+// critical path is U FMAs, the gates and the DPP broadcast.
+template <int U, int FS>
+__device__ __forceinline__ void chain_cell(const float (&cw)[3][FS + 2 * U], const float (&cb)[3],
+                                           const float (&cp)[4], int r, int j, const float* xin,
+                                           const float* hrow, float* xe, float* xe_g, float* st_g) {
+  constexpr int NI = FS + 2 * U, K = kD / FS, NP = FS + U;
+  float zp[K][3], ctk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float v[NP];
+#pragma unroll
+    for (int i = 0; i < FS; ++i) v[i] = xin[r * kD + k * FS + i];          // x_k
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[FS + u] = hrow[2 * U * k + U + u];        // m_time
+    ctk[k] = hrow[2 * U * k + j];                                           // c_time
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      float acc = cb[m];
+#pragma unroll
+      for (int i = 0; i < NP; ++i) acc = fmaf(v[i], cw[m][i], acc);
+      zp[k][m] = acc;
     }
   }
+  float cf = 0.f, mf[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) mf[u] = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float z[3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      float acc = zp[k][m];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = fmaf(mf[u], cw[m][NP + u], acc);  // m_freq of block k - 1
+      z[m] = acc;
+    }
+    const CellGates gt = cell_gates(z[0], z[1], z[2], cf, ctk[k], cp);   // coupled: f = 1 - i
+    const float cfn = gt.cfn, ctn = gt.ctn, mfn = gt.mfn, mtn = gt.mtn;
+    st_g[r * kD + 2 * U * k + j] = ctn;
+    st_g[r * kD + 2 * U * k + U + j] = mtn;
+    xe[r * kD + 2 * U * k + j] = mtn;
+    xe[r * kD + 2 * U * k + U + j] = mfn;
+    xe_g[r * kD + 2 * U * k + j] = mtn;
+    xe_g[r * kD + 2 * U * k + U + j] = mfn;
+    cf = cfn;
+    units_bcast<U>(mf, mfn);
+  }
+}
+
+template <int TPW, int U, int FS>
+__global__ void __launch_bounds__(kNT) g2k_encoder_chain_kernel(ChainArgs a) {
+  constexpr int H = 64 * TPW;          // Recur<TPW, 4>: four waves of 16 TPW columns
+  constexpr int HP = H + 4;            // h's LDS pitch: rows 4q + i of a lane group in distinct banks
+  constexpr int NI = FS + 2 * U;
+  constexpr int XR = (kD + 2) * kD;    // one frame's X / Xe
+  __shared__ __attribute__((aligned(16))) float sH[kD * HP];
+  __shared__ __attribute__((aligned(16))) float sXin[2][XR];
+  __shared__ __attribute__((aligned(16))) float sXe[kD * kD];
+  __shared__ __attribute__((aligned(16))) float sAs[kD * kD];
+  __shared__ __attribute__((aligned(16))) float sRed[4 * 16 * 4];
+  __shared__ float sWv[kT * (kD + 2)], sBv[kD], sWc[kL2 * kT], sWo[kT * kMaxN];
+  __shared__ float sG[kD * kT], sRm[kT * kD], sE[kT * kD], sC[kT * kT], sM[kL2 * kT];
+  const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), q = lane >> 4, L = lane & 15;
+  const int Nmax = a.f.d.Nmax;
+  const g2k_weights& w = a.f.w;
+  for (int i = tid; i < kT * (kD + 2); i += kNT) sWv[i] = w.Wv[i];
+  if (tid < kD) sBv[tid] = w.bv[tid];
+  if (tid < kL2 * kT) sWc[tid] = w.Wc[tid];
+  for (int i = tid; i < kT * Nmax; i += kNT) sWo[i] = w.Wo[i];
+  for (int i = tid; i < kD * H; i += kNT) sH[(i / H) * HP + (i % H)] = a.h[i];
+  const bool cell_lane = tid < kD * U;                 // wave 0
+  const int cr = tid / U, cj = tid - (tid / U) * U;
+  const bool peep = a.g.peep != nullptr;
+  float cw[3][NI], cb[3], cp[4];   // cw: the x_k, m_time terms first, then m_freq (chain_cell)
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    cb[m] = cell_lane ? a.g.b[m * U + cj] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) cw[m][i] = cell_lane ? a.g.W[i * 3 * U + m * U + cj] : 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) cp[m] = (cell_lane && peep) ? a.g.peep[m * U + cj] : 0.f;
+
+  // pred_path_band = M @ Wo of a finished frame (g2k_lstm_mcr.py:124)
+  auto pred_of = [&](size_t psf, int pnact, int t0, int nt) {
+    float* pp = a.pred + psf * kL2 * Nmax;
+    for (int i = t0; i < kL2 * Nmax; i += nt) {
+      const int jr = i / Nmax, n = i - jr * Nmax;
+      float x = 0.f;
+      if (n < pnact)
+        for (int t = 0; t < kT; ++t) x = fmaf(sM[jr * kT + t], sWo[t * Nmax + n], x);
+      pp[i] = x;
+    }
+  };
+  int64_t pend_sf = -1;
+  int pend_nact = 0;
+#ifdef G2K_CHAIN_STAMPS   // development probe (tools/probes/chain_stamps.py): phase cycles into cost[.][32..41]
+  uint64_t stamp[10];
+#define CHAIN_STAMP(k) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); stamp[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define CHAIN_STAMP(k) do { } while (0)
+#endif
+  for (int s = 0; s < a.S; ++s) {
+    const int nf = clampi(a.n_frames[s], 0, a.F);
+    if (nf == 0) continue;
+    const int nact = clampi(a.n_active[s], 0, Nmax);
+    const size_t sf0 = (size_t)s * a.F;
+    for (int i = tid; i < XR; i += kNT) sXin[0][i] = a.X[sf0 * XR + i];
+    if (tid < kD * kT) sG[tid] = a.f.lambda * a.G[(size_t)s * kD * kT + tid];
+    if (tid < kT * kD) {                               // Rm = Wr @ Rel (per batch)
+      const int t = tid / kD, dc = tid - t * kD;
+      const float* rel = a.Rel + (size_t)s * 2 * kD;
+      sRm[tid] = fmaf(w.Wr[2 * t], rel[dc], w.Wr[2 * t + 1] * rel[kD + dc]);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int f = 0; f < nf; ++f) {
+      const size_t sf = sf0 + f;
+      const bool more = f + 1 < nf;
+      CHAIN_STAMP(0);
+      float px0 = 0.f, px1 = 0.f;                      // the next frame's X, parked in step 4
+      if (more) {
+        px0 = a.X[(sf + 1) * XR + tid];
+        if (tid < XR - kNT) px1 = a.X[(sf + 1) * XR + kNT + tid];
+      }
+      // 1. h rows' maxima; the cell (train.py:201-207) | the previous frame's pred
+      Recur<TPW, 4> rec;
+      rec.load(sH, HP, wv, q, L);
+      rec.init_max(sRed + 192, wv, q, L);
+      CHAIN_STAMP(1);
+      if (wv == 0) {
+        if (cell_lane)
+          chain_cell<U, FS>(cw, cb, cp, cr, cj, sXin[cur], sH + cr * HP, sXe, a.Xe + sf * XR,
+                            a.g.state_out);
+      } else if (pend_sf >= 0) {
+        pred_of((size_t)pend_sf, pend_nact, tid - 64, kNT - 64);
+      }
+      CHAIN_STAMP(2);
+      __syncthreads();
+      CHAIN_STAMP(3);
+      // 2. E = Wv @ X + bv (g2k_lstm_mcr.py:99-124); softmax numerators of h
+      if (tid < kT * kD) {
+        const int t = tid / kD, dc = tid - t * kD;
+        float e = 0.f;
+#pragma unroll
+        for (int k = 0; k < kD + 2; ++k)
+          e = fmaf(sWv[t * (kD + 2) + k], k < kD ? sXe[k * kD + dc] : sXin[cur][k * kD + dc], e);
+        sE[tid] = e + sBv[dc];
+      }
+      rec.init_exp(sRed, sRed + 192, wv, q, L);
+      __syncthreads();
+      CHAIN_STAMP(4);
+      // 3. A = g @ (E * Rm), cost = E @ g
+      {
+        const int r = tid / kD, dc = tid - r * kD;
+        float x = 0.f;
+        for (int t = 0; t < kT; ++t) x = fmaf(sG[r * kT + t], sE[t * kD + dc] * sRm[t * kD + dc], x);
+        a.attn[sf * kD * kD + tid] = x;
+        sAs[tid] = x;
+      }
+      if (tid < kT * kT) {
+        const int t1 = tid >> 3, t2 = tid & 7;
+        float c = 0.f;
+        for (int k = 0; k < kD; ++k) c = fmaf(sE[t1 * kD + k], sG[k * kT + t2], c);
+        sC[tid] = c;
+        a.cost[sf * kT * kT + tid] = c;
+      }
+      __syncthreads();
+      CHAIN_STAMP(5);
+      // 4. As (train.py:240) on wave 0 | M = Wc @ cost on waves 1..3; next X parked
+      if (more) {
+        sXin[cur ^ 1][tid] = px0;
+        if (tid < XR - kNT) sXin[cur ^ 1][kNT + tid] = px1;
+      }
+      if (wv == 0) {
+        attn_tile_wave(sAs, kD, lane);
+        CHAIN_STAMP(6);
+      } else {
+        const int i = tid - 64, jr = i >> 3, t2 = i & 7;
+        float x = 0.f;
+        for (int t = 0; t < kT; ++t) x = fmaf(sWc[jr * kT + t], sC[t * kT + t2], x);
+        sM[i] = x;
+      }
+      __syncthreads();
+      CHAIN_STAMP(7);
+      // 5. the recurrence frame (train.py:243-252; its barrier inside), h back to LDS
+      const float4 b = *reinterpret_cast<const float4*>(sAs + L * kD + 4 * q);
+      rec.step(b, sRed, sRed + 64, wv, q, L);
+      CHAIN_STAMP(8);
+      rec.store(sH, HP, wv, q, L, sRed + 64);
+      pend_sf = (int64_t)sf;
+      pend_nact = nact;
+      cur ^= 1;
+      __syncthreads();
+      CHAIN_STAMP(9);
+#ifdef G2K_CHAIN_STAMPS
+      if (tid == 0)
+        for (int k = 1; k < 10; ++k) a.cost[sf * kT * kT + 32 + k] = (float)(stamp[k] - stamp[k - 1]);
+#endif
+    }
+  }
+  if (pend_sf >= 0) pred_of((size_t)pend_sf, pend_nact, tid, kNT);
+  for (int i = tid; i < kD * H; i += kNT) a.h[i] = sH[(i / H) * HP + (i % H)];
 }
 
 // ---------------------------------------------------------------------------

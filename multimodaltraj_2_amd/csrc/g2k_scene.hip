@@ -167,18 +167,6 @@ struct FrameHeadOut {
   f32x4 mT0, mT1;   // M[L][4q+i] (x rows), M[12+L][4q+i] (y rows)
 };
 
-// Partner lane's value across lane groups (q ^ 1 by permlane16, q ^ 2 by
-// permlane32): of the pair a swap returns, one element is this lane's own
-// value, the other the partner's.
-__device__ __forceinline__ float partner16(float v) {
-  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return a[0] == __float_as_uint(v) ? __uint_as_float(a[1]) : __uint_as_float(a[0]);
-}
-__device__ __forceinline__ float partner32(float v) {
-  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return a[0] == __float_as_uint(v) ? __uint_as_float(a[1]) : __uint_as_float(a[0]);
-}
-
 // As = softmax(exp(A) / cumsum(exp(A), axis 0), axis -1)  (train.py:240) of
 // one frame's A in the MFMA result layout (column L, rows 4q + i), written
 // to as_dst [16][16].  The ratio exp(A_r) / sum_{k<=r} exp(A_k) is invariant

@@ -70,7 +70,11 @@ def test_chain_entry_bit_identical_to_python_loop(gpu, H):
 
 def test_chain_entry_time_per_frame(gpu):
     """The one-workgroup chain against the Python loop of launches over the
-    same 160 frames (timing printed; the chain kernel must not be slower)."""
+    same 160 frames (timing printed; the chain kernel must not be slower).
+    Wall time per frame including the entry point's host work and its
+    embed / error launches: 12.2 us in round 5 (global hand-offs between
+    barriers), 3.4 us with every hand-off in LDS (profiles/r11e_chain_stamps.txt);
+    the bound below is a regression guard with room for box-to-box spread."""
     S, F = 8, 20
     t, n_frames, G, params, cell, h0 = setup(gpu, S, F)
     n_frames = torch.full((S,), F, dtype=torch.int32, device=gpu)
@@ -97,3 +101,4 @@ def test_chain_entry_time_per_frame(gpu):
         res[name] = best / (S * F) * 1e6
     print(json.dumps({"us_per_frame": res, "frames": S * F}))
     assert res["chain_kernel"] <= res["python_loop"]
+    assert res["chain_kernel"] <= 6.0
