@@ -243,13 +243,14 @@ __device__ __forceinline__ void attn_weights(const f32x4 aA, float* as_dst, int 
 // A contracts over t = 4q + ks (rows of E as the MFMA left them).  As goes
 // to `as_dst`; cost to `cost_g` (global, krnl_mdl.cost) and / or `cost_l`
 // (LDS, train mode); the x / y row tiles of M^T are returned (M[L][4q+i]).
-template <bool PAD>
+template <bool PAD, bool REP = false>
 __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float* sV,
                                                    const float* sVG, int wrow0, int wcmax,
                                                    const float (&rm)[4], float lam, float* as_dst,
                                                    int* as_flag, int flag_val, float* A_g,
                                                    float* cost_g, float* cost_l, int L, int q,
-                                                   bool want_m = true, bool want_as = true) {
+                                                   bool want_m = true, bool want_as = true,
+                                                   int nrep = 1) {
   // every operand load is unconditional and issued before the first MFMA.
   // PAD: the LDS operands are zero-padded to the 16 lanes (K1, K2, lambda G,
   // VG columns; the augmented rows Ve0, Ve1, bv, 0 of V and VG), so no lane
@@ -341,9 +342,15 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
       o.mT1 = mfma4(va[ks], by[ks], o.mT1);   // M[12+L][4q+i]    (y rows)
     }
   }
-  if (A_g && want_as) {
+  if (A_g && want_as) {   // (REP: the same A for nrep consecutive frames, frames_invariant)
+    if constexpr (REP) {
+      for (int r = 0; r < nrep; ++r)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) A_g[(4 * q + i) * kD + L] = aA[i];
+        for (int i = 0; i < 4; ++i) A_g[r * kD * kD + (4 * q + i) * kD + L] = aA[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) A_g[(4 * q + i) * kD + L] = aA[i];
+    }
   }
   if (cost_g || cost_l) {
     f32x4 cC = {0.f, 0.f, 0.f, 0.f};
@@ -352,7 +359,13 @@ __device__ __forceinline__ FrameHeadOut frame_head(const float* sm, const float*
     if (q < 2 && L < kT) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (cost_g) cost_g[(4 * q + i) * kT + L] = cC[i];
+        if (cost_g) {
+          if constexpr (REP) {
+            for (int r = 0; r < nrep; ++r) cost_g[r * kT * kT + (4 * q + i) * kT + L] = cC[i];
+          } else {
+            cost_g[(4 * q + i) * kT + L] = cC[i];
+          }
+        }
         if (cost_l) cost_l[(4 * q + i) * kT + L] = cC[i];
       }
     }
@@ -607,9 +620,10 @@ __device__ __forceinline__ void scene_rm(const SceneLayout& lay, const SceneCtx&
 // prediction tiles, round 4: kfold4 10.8 -> 10.6 us per step, relational
 // 18.7 -> 18.4, the 2-tile shapes neutral — right after the first staging;
 // the scene's recurrence workgroup)
-template <bool CR>
+template <bool CR, bool INV>
 __device__ __forceinline__ int rec_head_frames(const SceneLayout& lay, const SceneCtx& c) {
   const int n = c.nf < lay.fc ? c.nf : lay.fc;
+  if (INV) return n < 1 ? n : 1;              // loop-invariant frames: frame 0's head only
   const int m = kRecW * (CR && c.ntact >= 3 ? 2 : 1);
   return n < m ? n : m;
 }
@@ -658,7 +672,7 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
 // HBM burst, which every wave's B1 waits for, stays free of it) and its
 // softmax numerators are formed there too; after B2 the waves form As of the
 // first frames themselves and start the chain.
-template <int TPW, int NP, bool CR, bool PAD>
+template <int TPW, int NP, bool CR, bool PAD, bool INV>
 __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneLayout& lay,
                                                  const SceneCtx& c) {
   constexpr int NT = 64 * (kRecW + NP);
@@ -689,7 +703,7 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
   // priority: the producers reach their first heads only after their loop
   // set-up (thousands of cycles of scalar work on the CU's one scalar unit);
   // they form only M for these frames
-  for (int fl = c.wv; live && fl < rec_head_frames<CR>(lay, c); fl += kRecW) {
+  for (int fl = c.wv; live && fl < rec_head_frames<CR, INV>(lay, c); fl += kRecW) {
     __builtin_amdgcn_s_setprio(3);
     float rm[4];
     scene_rm(lay, c, rm);
@@ -700,11 +714,12 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     // be published before that cost is in LDS
     constexpr bool kRecM = CR;
     const FrameHeadOut hd =
-        frame_head<PAD>(c.sm, c.sV, c.sVG, fl * a.d.stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
+        frame_head<PAD, INV>(c.sm, c.sV, c.sVG, fl * a.d.stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                    c.sFlag + fl, fl + 1,
                    a.A_out && mine ? a.A_out + ((size_t)c.s * a.d.F + fl) * kD * kD : nullptr,
                    kRecM && a.cost_out && mine ? a.cost_out + ((size_t)c.s * a.d.F + fl) * kT * kT : nullptr,
-                   nullptr, c.L, c.q, /*want_m=*/kRecM && mine);
+                   nullptr, c.L, c.q, /*want_m=*/kRecM && mine, true,
+                   INV ? (c.nf < lay.fc ? c.nf : lay.fc) : 1);
     if (kRecM && mine) {
       if (c.L < kL && c.q < 2) {
         float* m = c.sMring + fl * kL2 * kT;
@@ -722,7 +737,24 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
       scene_pos_dma<NT>(a, lay, c, fb, cnt);
       scene_stage<NT, NP, PAD>(a, lay, c, fb, cnt, [] {});
     }
-    if (live) {
+    if (INV && live) {
+      // loop-invariant frames: the chunk's one As (its local frame 0's slot,
+      // flagged fb + 1) for every frame; the chain itself is unchanged
+      __builtin_amdgcn_s_setprio(2);
+      const float* as_lane = c.sRing + c.L * kD + 4 * c.q;
+      float4 b;
+      wait_as(c.sFlag, fb + 1, as_lane, b);
+      for (int fl = 0; fl < cnt; ++fl) {
+        const int g = fb + fl;
+        f32x4 z;
+        poll_red(seq + (c.L & 3), g + 2, c.sRed + (g & 1) * kRB + (c.L & 3) * 16 + 4 * c.q, z);
+        int fln;
+        float4 bn;
+        rc.step_seq(b, z, c.sRed + ((g + 1) & 1) * kRB, seq, g + 3, c.wv, c.q, c.L, c.sFlag, as_lane,
+                    fln, bn, g + 1 == c.nf);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    } else if (live) {
       __builtin_amdgcn_s_setprio(2);
       const float* as_lane = c.sRing + c.L * kD + 4 * c.q;   // this lane's As row quad, ring slot 0
       // one frame; (b, flq): this frame's prefetched As quad and flag, (bn,
@@ -821,12 +853,16 @@ __device__ __forceinline__ void nll_pairs(const float* sC, float* sA, int q, boo
   }
 }
 
-template <bool GRAD, bool PM, bool NLL, typename AfterTargets>
+// REP (forward, frames_invariant): the tile stands for `nrep` frames with the
+// same values — its stores are repeated at `pr`'s consecutive frames and its
+// a9 terms enter the sums with weight nrep (the count with nrep pairs).
+template <bool GRAD, bool PM, bool NLL, bool REP = false, typename AfterTargets>
 __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, float* ys, brsrc pr,
                                           const float2 (&tg)[4], bool has_t, int Nmax, int nact,
                                           int t, int L, int q, float acc[5], float& lsum,
                                           f32x4 (&dm)[2], f32x4& dWoT, AfterTargets after_targets,
-                                          const float* nllC = nullptr, float* nllA = nullptr) {
+                                          const float* nllC = nullptr, float* nllA = nullptr,
+                                          int nrep = 1) {
   if (GRAD && NLL) asm volatile("" : "+v"(L), "+v"(q));   // (as in frame_grad<OPAQUE>)
   const int n0 = 16 * t, n = n0 + L;
   const bool hi = q < 2;                                   // block-1 rows exist (r < 24)
@@ -867,8 +903,25 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
     // stores at the offsets of its two target loads; pedestrians >= n_active
     // are not written (a contiguous n_active * 96-byte run per frame)
     const int off = n * kL2 * 4;
-    bstore4(pr, n < nact ? off + 16 * q : kBufOff, y0[0], y0[1], y0[2], y0[3]);
-    bstore4(pr, (n < nact && hi) ? off + 64 + 16 * q : kBufOff, y1[0], y1[1], y1[2], y1[3]);
+    if constexpr (REP) {
+      for (int r = 0; r < nrep; ++r) {
+        const int fo = r * (kL2 * Nmax * 4);
+        bstore4(pr, n < nact ? fo + off + 16 * q : kBufOff, y0[0], y0[1], y0[2], y0[3]);
+        bstore4(pr, (n < nact && hi) ? fo + off + 64 + 16 * q : kBufOff, y1[0], y1[1], y1[2], y1[3]);
+      }
+    } else {
+      bstore4(pr, n < nact ? off + 16 * q : kBufOff, y0[0], y0[1], y0[2], y0[3]);
+      bstore4(pr, (n < nact && hi) ? off + 64 + 16 * q : kBufOff, y1[0], y1[1], y1[2], y1[3]);
+    }
+  } else if constexpr (REP) {
+    for (int r = 0; r < nrep; ++r) {
+      const int fo = r * (kL2 * Nmax * 4);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        bstore(pr, n < Nmax ? fo + (mrow(4 * q + v) * Nmax + n) * 4 : kBufOff, y0[v]);
+        bstore(pr, (n < Nmax && hi) ? fo + (mrow(16 + 4 * q + v) * Nmax + n) * 4 : kBufOff, y1[v]);
+      }
+    }
   } else {
     // range-checked 4-byte stores (no branch): the block-1 rows of lane
     // groups 2, 3 and columns past Nmax fall outside the frame's buffer.  The
@@ -910,7 +963,8 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
   }
   // el2 needs no sum across lanes: each lane adds its steps' share (the
   // lanes are summed when the metrics are published)
-  acc[3] = fmaf(has_t ? 1.0f / 12.0f : 0.f, el2, acc[3]);
+  const float wrep = REP ? (float)nrep : 1.f;
+  acc[3] = fmaf(has_t ? wrep * (1.0f / 12.0f) : 0.f, el2, acc[3]);
   // ea, eb, ec summed over the four lane groups and gathered in group 1 (it
   // holds step 11, the fde) by five permlane swaps, branch-free after.
   // permlane32_swap(x, y) -> {[x.lo, y.lo], [x.hi, y.hi]} (32-lane halves);
@@ -930,7 +984,7 @@ __device__ __forceinline__ void pred_tile(const float* M, const float* sWo, floa
   const auto p5 = sw32(__uint_as_float(p4[0]), __uint_as_float(p4[0]));   // [1]: eb everywhere
   const float sa = __uint_as_float(p4[0]), sb = __uint_as_float(p5[1]), sc = tt;   // row 1
   {
-    const float g1 = (has_t && q == 1) ? 1.f : 0.f;   // group 1's lanes of pedestrians with targets
+    const float g1 = (has_t && q == 1) ? wrep : 0.f;   // group 1's lanes of pedestrians with targets
     const float fx = d1[2], fy = d1[3];
     const float hm = 0.5f * (sa - sc);
     const float lam = 0.5f * (sa + sc) + __builtin_amdgcn_sqrtf(fmaf(hm, hm, sb * sb));
@@ -1432,7 +1486,7 @@ __device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCt
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
-template <int NP, bool GRAD, bool PM, bool NLL, bool CR>
+template <int NP, bool GRAD, bool PM, bool NLL, bool CR, bool INV>
 __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLayout& lay,
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
@@ -1482,7 +1536,8 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
     const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
     ofo = own.fo;
-    const int nitems = own.n * ntact > pw ? (own.n * ntact - pw + NP - 1) / NP : 0;   // forward
+    const int nown = INV ? (own.n < 1 ? own.n : 1) : own.n;   // (INV: frame 0 only)
+    const int nitems = nown * ntact > pw ? (nown * ntact - pw + NP - 1) / NP : 0;   // forward
     // GRAD: this producer's own frames (ordinals) pw, pw + NP, ... < gend of
     // the chunk (the last R own frames of the last chunk go to the
     // recurrence waves)
@@ -1506,8 +1561,10 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // (and A / cost out) only for own frames.  The recurrence waves form As
     // of the first chunk's frames 0 .. nrh - 1 themselves (M only here).
     const bool all_heads = a.h_in != nullptr && c.x == 0;
-    const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : c.X, nh = all_heads ? cnt : own.n;
-    const int nrh = all_heads && fb == 0 ? rec_head_frames<CR>(lay, c) : 0;
+    const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : c.X,
+              nh = all_heads ? (INV ? (cnt < 1 ? cnt : 1) : cnt) : own.n;
+    const int nrep = INV ? cnt : 1;              // frames one head / tile stands for
+    const int nrh = all_heads && fb == 0 ? rec_head_frames<CR, INV>(lay, c) : 0;
     for (int i = pw; i < nh; i += NP) {
       const int fl = hb + hs * i;
       const int f = fb + fl;
@@ -1520,11 +1577,11 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       if (CR) __builtin_amdgcn_s_setprio(2);
       else if (fl >= nrh && fl < NP + nrh) __builtin_amdgcn_s_setprio(1);   // the first round's heads
       const FrameHeadOut hd =
-          frame_head<!GRAD>(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
+          frame_head<!GRAD, INV>(c.sm, c.sV, c.sVG, fl * stride, lay.wcmax, rm, a.lambda, c.sRing + fl * kD * kD,
                      c.sFlag + fl, f + 1,
                      a.A_out && mine ? a.A_out + ((size_t)s * F + f) * kD * kD : nullptr,
                      a.cost_out && mine ? a.cost_out + ((size_t)s * F + f) * kT * kT : nullptr,
-                     GRAD ? c.sCost + fl * kT * kT : nullptr, L, q, mine, fl >= nrh);
+                     GRAD ? c.sCost + fl * kT * kT : nullptr, L, q, mine, fl >= nrh, nrep);
       if (mine) {
         if (L < kL && q < 2) {
           float* m = c.sMring + fl * kL2 * kT;
@@ -1565,12 +1622,30 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
                                     (act_bits >> t) & 1u, Nmax, c.nact, t, L, q, acc, lsum, dm,
                                     dWoT, [] {});
       };
-      for (int k = 0; k < nitems; k += kNB) {
+      if constexpr (INV) {
+        auto item_inv = [&](int k, float2 (&tg)[4]) {   // the chunk's frames at once
+          int fl, t;
+          item_ft(k, fl, t);
+          poll_flag(c.sMflag + fl, fb + fl + 1);
+          const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)s * F + fb) * kL2 * Nmax : a.targets,
+                                      a.pred ? (uint32_t)(cnt * kL2 * Nmax * 4) : 0u);
+          f32x4 dWoT;
+          // (the next item's targets go out once this one's are consumed, ahead
+          // of the stores, as in the train tiles)
+          pred_tile<false, PM, false, true>(c.sMring + fl * kL2 * kT, c.sWo, c.sY, pr, tg,
+                                            (act_bits >> t) & 1u, Nmax, c.nact, t, L, q, acc, lsum, dm,
+                                            dWoT, [&] { load_item(fb, nitems, k + 1, tg); }, nullptr,
+                                            nullptr, cnt);
+        };
+        for (int k = 0; k < nitems; ++k) item_inv(k, tg[0]);
+      } else {
+        for (int k = 0; k < nitems; k += kNB) {
 #pragma unroll
-        for (int j = 0; j < kNB; ++j) {
-          if (k + j < nitems) {
-            item(k + j, tg[j]);
-            load_item(fb, nitems, k + j + kNB, tg[j]);
+          for (int j = 0; j < kNB; ++j) {
+            if (k + j < nitems) {
+              item(k + j, tg[j]);
+              load_item(fb, nitems, k + j + kNB, tg[j]);
+            }
           }
         }
       }
@@ -1729,7 +1804,7 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
 template <int TPW, int NP>
 constexpr int scene_waves_per_eu() { return NP == 4 && TPW < 8 ? 4 : 1; }
 
-template <int TPW, int NP, bool GRAD, bool PM, bool NLL>
+template <int TPW, int NP, bool GRAD, bool PM, bool NLL, bool INV>
 __global__ void __launch_bounds__(64 * (kRecW + NP))
 __attribute__((amdgpu_waves_per_eu(scene_waves_per_eu<TPW, NP>())))
 g2k_scene_kernel(StepArgs a, SceneLayout lay) {
@@ -1841,11 +1916,11 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   };
   if (c.wv < kRecW) {
     scalars();
-    scene_recurrence<TPW, NP, CR, !GRAD>(a, lay, c);
+    scene_recurrence<TPW, NP, CR, !GRAD, INV>(a, lay, c);
     if (GRAD) rec_grad_work<NP, PM, NLL>(a, lay, c);
   } else {
     scalars();
-    scene_producer<NP, GRAD, PM, NLL, CR>(a, lay, c);
+    scene_producer<NP, GRAD, PM, NLL, CR, INV>(a, lay, c);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
 }
@@ -1873,14 +1948,27 @@ int scene_producers(const g2k_dims& d, int H, bool grad) {
   return 12;
 }
 
+// Every frame of a scene has the same inputs: stride 0 (each frame reads the
+// same window rows) and one target set for every frame
+// (G2K_STEP_TARGETS_SHARED) — sample.py's time-slice scenes, the train.py
+// legs.  E, A, As, cost, M, Y and the a9 terms are then the same in every
+// frame and only h changes along them, so the forward (g2k_scene_kernel<...,
+// INV>, one workgroup per scene) forms one head and one set of tiles per chunk
+// and replicates their outputs over the chunk's frames.
+inline bool frames_invariant(const g2k_dims& d, const SceneLayout& l) {
+  return d.stride == 0 && l.tfb == 0 && l.split == 1;
+}
+
 template <int TPW, int NP, bool GRAD, bool PM>
 void launch_kp(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
   const dim3 grid(a.d.S * l.split), block(64 * (kRecW + NP));
   const size_t lds = (size_t)l.total * 4;
   if (GRAD && loss_nll(a.d))
-    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, GRAD>), grid, block, lds, st, a, l);
+    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, GRAD, false>), grid, block, lds, st, a, l);
+  else if (!GRAD && frames_invariant(a.d, l))
+    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, !GRAD>), grid, block, lds, st, a, l);
   else
-    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false>), grid, block, lds, st, a, l);
+    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, false>), grid, block, lds, st, a, l);
 }
 
 template <int TPW, int NP, bool GRAD>

@@ -66,6 +66,42 @@ def test_shared_targets_equal_replicated(gpu):
         np.testing.assert_array_equal(getattr(got, k).cpu().numpy(), getattr(ref, k).cpu().numpy())
 
 
+@pytest.mark.parametrize("layout,coresident", [("band", False), ("ped", False), ("ped", True)])
+def test_invariant_frames_equal_general_path(gpu, layout, coresident):
+    """Stride 0 with shared targets and one workgroup per scene: every frame
+    has the same inputs, and the forward forms one head and one set of tiles
+    per chunk and replicates them (g2k_scene.hip frames_invariant).  Against
+    the general path on the same frames (replicated targets): pred, h, attn
+    and cost bit-identical (the same arithmetic per frame); the metric sums
+    within 1e-6 relative (n_frames x one frame's terms instead of a sum over
+    frames).  F = 40: two chunks of frames (kSceneChunk = 32)."""
+    S, F = 24, 40
+    b = make_batch(S, 32, 128, F=F, seed=11)
+    t = b.to_device(gpu)
+    pos = t["pos"][:, :8].contiguous()
+    tgt1 = t["targets"][:, :1].contiguous()
+    nf = torch.from_numpy(np.random.default_rng(4).integers(0, F + 1, S).astype(np.int32)).to(gpu)
+    nf[0], nf[1] = F, 33                                   # both chunks, a 1-frame second chunk
+    params = fs.init_params(32, seed=0, device=gpu)
+    kw = dict(n_frames=nf, stride=0, want_attn=True, pred_layout=layout, split=1)
+    ref = fs.step_fused(params, pos, t["vislet"], t["G"], tgt1.expand(-1, F, -1, -1, -1).contiguous(),
+                        t["n_active"], t["h0"], **kw)
+    got = fs.step_fused(params, pos, t["vislet"], t["G"], tgt1, t["n_active"], t["h0"],
+                        targets_shared=True, frames=F, coresident=coresident, **kw)
+    torch.cuda.synchronize()
+    nfh = nf.cpu().numpy()
+    for s in range(S):
+        n, f = int(b.n_active[s]), int(nfh[s])
+        gp, rp = fs.pred_band(got.pred, layout)[s, :f, :, :n], fs.pred_band(ref.pred, layout)[s, :f, :, :n]
+        assert torch.equal(gp, rp), s
+        assert torch.equal(got.attn[s, :f], ref.attn[s, :f]) and torch.equal(got.cost[s, :f], ref.cost[s, :f]), s
+    assert torch.equal(got.h, ref.h)
+    gm, rm = got.metrics.cpu().numpy(), ref.metrics.cpu().numpy()
+    assert np.abs(gm - rm).max() <= 1e-6 * max(1.0, np.abs(rm).max())
+    np.testing.assert_array_equal(gm[:, 1], rm[:, 1])      # the pair counts
+    np.testing.assert_array_equal(gm[:, 5], rm[:, 5])      # frames
+
+
 @pytest.mark.parametrize("layout,shared", [("ped", False), ("band", True), ("ped", True)])
 def test_train_step_layouts_equal_default(gpu, layout, shared):
     b, t, F = _shared_batch(gpu)

@@ -41,12 +41,20 @@ def test_device_gather_equals_host_expansion(plan, dev_batch):
         np.testing.assert_array_equal(dev_batch[k].cpu().numpy(), h[k], err_msg=k)
 
 
-def test_every_real_scene_matches_oracle(gpu, plan, dev_batch):
+@pytest.mark.parametrize("shared", [False, True])
+def test_every_real_scene_matches_oracle(gpu, plan, dev_batch, shared):
+    """shared: one target set per scene (G2K_STEP_TARGETS_SHARED) and one
+    co-resident workgroup per scene — bench.py's real-data launch, which runs
+    the loop-invariant forward (stride 0: one head and one set of tiles per
+    chunk, replicated over the frames; g2k_scene.hip frames_invariant)."""
     t = dev_batch
     Nmax = plan.Nmax
     params = fs.init_params(Nmax, seed=0, device=gpu)
-    out = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"], t["h0"],
-                      n_frames=t["n_frames"], ped_mask=t["ped_mask"], stride=0).run()
+    tgt = t["targets"][:, :1].contiguous() if shared else t["targets"]
+    out = fs.StepPlan(params, t["pos"], t["vislet"], t["G"], tgt, t["n_active"], t["h0"],
+                      n_frames=t["n_frames"], ped_mask=t["ped_mask"], stride=0,
+                      targets_shared=shared, frames=int(t["targets"].shape[1]) if shared else None,
+                      coresident=shared).run()
     torch.cuda.synchronize()
     h = plan.host()
     G = t["G"].cpu().numpy()
