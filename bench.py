@@ -510,10 +510,14 @@ def main(argv=None):
     ap.add_argument("--split", type=int, default=0,
                     help="workgroups per scene (G2K_STEP_SPLIT; 0: automatic, enough to cover "
                          "the CUs when a rank has fewer scenes than CUs)")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=16,
                     help="reference mode: consecutive (independent) batches on this many "
                          "streams in turn, so launches overlap (the roofline still divides by "
-                         "one launch's duration)")
+                         "one launch's duration).  16: the timed steps' launches are all queued "
+                         "at once, so a CU's freed workgroup slot is refilled from the next "
+                         "launch at once (profiles/r11m_streams_sweep.txt: eth_hotel_synth "
+                         "14.3 -> 13.7-13.9 us per step at 20 steps against 4 streams, 12.5 -> "
+                         "11.8 at 200; every config gains)")
     ap.add_argument("--coresident", choices=("auto", "on", "off"), default="auto",
                     help="reference mode: G2K_STEP_CORESIDENT (two 8-wave workgroups per CU "
                          "while launches are in flight); auto = on with 2 or more streams")
@@ -674,7 +678,7 @@ def main(argv=None):
                                                              args.split, cores),
                        "coresident": cores,
                        "workgroups_per_cu": fs.step_coresidency(S, F, H, Nmax, b.pos.shape[1], b.stride,
-                                                                cores),
+                                                                cores, shared),
                        "streams": len(streams),
                        "launch": "host launch per step" if args.no_graph else
                                  "HIP graph of the timed steps (one replay)"},

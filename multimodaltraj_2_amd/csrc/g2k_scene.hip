@@ -89,7 +89,7 @@ struct SceneLayout {
 };
 
 __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int F, int fc, int NP,
-                                                       bool grad, bool nll = false) {
+                                                       bool grad, bool nll = false, bool inv = false) {
   SceneLayout s;
   s.fc = fc;
   s.split = 1;
@@ -107,8 +107,9 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   const int NG = NP + kRecW;                          // train: producers + recurrence waves
   s.o_y = o;     o += grad ? NG * kL2 * kYP : 0;      // dY tile scratch (train)
   s.o_met = o;   o += (grad ? NG : NP) * 8;
-  s.o_ring = o;  o += fc * kD * kD;
-  s.o_mring = o; o += fc * kL2 * kT;                  // M = Wc @ cost per frame [24][8]
+  const int slots = inv ? 1 : fc;                     // (loop-invariant frames: one slot, frames_invariant)
+  s.o_ring = o;  o += slots * kD * kD;
+  s.o_mring = o; o += slots * kL2 * kT;               // M = Wc @ cost per frame [24][8]
   s.o_flag = o;  o += rup4(fc);                      // As ring flags (recurrence polls)
   s.o_mflag = o; o += rup4(fc);                      // M ring flags (prediction tiles poll)
   s.o_red = o;   o += 4 * 16 * kRecW;
@@ -138,13 +139,26 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   return s;
 }
 
+// Every frame of a scene has the same inputs: stride 0 (each frame reads the
+// same window rows) and one target set for every frame
+// (G2K_STEP_TARGETS_SHARED) — sample.py's time-slice scenes, the train.py
+// legs.  E, A, As, cost, M, Y and the a9 terms are then the same in every
+// frame and only h changes along them, so the forward (g2k_scene_kernel<...,
+// INV>, one workgroup per scene) forms one head and one set of tiles per chunk
+// and replicates their outputs over the chunk's frames; its rings hold one
+// slot.
+__host__ inline bool frames_invariant(const g2k_dims& d, bool grad) {
+  return !grad && d.stride == 0 && (d.flags & G2K_STEP_TARGETS_SHARED) && scene_split(d) == 1;
+}
+
 __host__ inline SceneLayout scene_layout(const g2k_dims* d, int NP, bool grad) {
   const bool nll = grad && loss_nll(*d);
+  const bool inv = frames_invariant(*d, grad);
   int fc = d->F < 1 ? 1 : (d->F < kSceneChunk ? d->F : kSceneChunk);
-  SceneLayout l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad, nll);
+  SceneLayout l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad, nll, inv);
   while ((int64_t)l.total * 4 > 160 * 1024 && fc > 1) {
     fc = (fc + 1) / 2;
-    l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad, nll);
+    l = scene_layout_fc(d->Nmax, d->stride, d->F, fc, NP, grad, nll, inv);
   }
   l.tfb = (d->flags & G2K_STEP_TARGETS_SHARED) ? 0 : d->Nmax * kL2 * 4;
   l.split = scene_split(*d);
@@ -1948,24 +1962,13 @@ int scene_producers(const g2k_dims& d, int H, bool grad) {
   return 12;
 }
 
-// Every frame of a scene has the same inputs: stride 0 (each frame reads the
-// same window rows) and one target set for every frame
-// (G2K_STEP_TARGETS_SHARED) — sample.py's time-slice scenes, the train.py
-// legs.  E, A, As, cost, M, Y and the a9 terms are then the same in every
-// frame and only h changes along them, so the forward (g2k_scene_kernel<...,
-// INV>, one workgroup per scene) forms one head and one set of tiles per chunk
-// and replicates their outputs over the chunk's frames.
-inline bool frames_invariant(const g2k_dims& d, const SceneLayout& l) {
-  return d.stride == 0 && l.tfb == 0 && l.split == 1;
-}
-
 template <int TPW, int NP, bool GRAD, bool PM>
 void launch_kp(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
   const dim3 grid(a.d.S * l.split), block(64 * (kRecW + NP));
   const size_t lds = (size_t)l.total * 4;
   if (GRAD && loss_nll(a.d))
     hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, GRAD, false>), grid, block, lds, st, a, l);
-  else if (!GRAD && frames_invariant(a.d, l))
+  else if (!GRAD && frames_invariant(a.d, false))
     hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, !GRAD>), grid, block, lds, st, a, l);
   else
     hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, false>), grid, block, lds, st, a, l);

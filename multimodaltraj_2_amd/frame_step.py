@@ -141,23 +141,24 @@ class StepOutputs:
     cost: torch.Tensor | None = None   # [S, F, T, T]
 
 
-def step_lds_bytes(S, F, H, Nmax, W, stride, coresident=False) -> int:
+def step_lds_bytes(S, F, H, Nmax, W, stride, coresident=False, targets_shared=False) -> int:
     lib = _lib.load()
     d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, H, Nmax, W, stride,
-                     step_flags(coresident=coresident))
+                     step_flags(coresident=coresident, targets_shared=targets_shared))
     return int(lib.g2k_step_lds_bytes(ctypes.byref(d)))
 
 
 CORESIDENT_LDS = 80 * 1024     # g2k_scene.hip kCoresidentLds
 
 
-def step_coresidency(S, F, H, Nmax, W, stride, coresident=False) -> int:
+def step_coresidency(S, F, H, Nmax, W, stride, coresident=False, targets_shared=False) -> int:
     """Workgroups of one step launch a CU holds at once: 2 under
     G2K_STEP_CORESIDENT when the 8-wave geometry applies (H < 512 and the
     scene's LDS fits twice, include/g2k_hip.h), else 1."""
     if not coresident or H >= 512:
         return 1
-    return 2 if step_lds_bytes(S, F, H, Nmax, W, stride, True) <= CORESIDENT_LDS else 1
+    lds = step_lds_bytes(S, F, H, Nmax, W, stride, True, targets_shared)
+    return 2 if lds <= CORESIDENT_LDS else 1
 
 
 def device_cus(device) -> int:
