@@ -232,3 +232,26 @@ def test_split_sizing_without_a_gpu_is_explicit():
         P = lib.g2k_grad_size(ctypes.byref(d))
         assert tb == 128 * x * (P + 2) * 4 + 64 + nb       # one gradient row per workgroup
     assert len(sizes) == 3
+
+
+def test_loop_invariant_launches_hold_one_ring_slot():
+    """Stride 0 with shared targets and one workgroup per scene
+    (g2k_scene.hip frames_invariant): the forward forms one head per chunk,
+    so its rings hold one slot — a smaller LDS carve-up than the same launch
+    with per-frame targets, whose rings hold every frame of the chunk; train
+    mode and split launches keep the general layout (host arithmetic, no
+    GPU)."""
+    from multimodaltraj_2_amd import frame_step as fs
+    lib = _lib.load()
+
+    def lds(F, shared, split, coresident=False, stride=0, W=8):
+        d = _lib.G2KDims(128, F, 8, 12, 16, 128, 32, W, stride,
+                         fs.step_flags(targets_shared=shared, split=split, coresident=coresident))
+        return lib.g2k_step_lds_bytes(ctypes.byref(d))
+
+    general, inv = lds(29, False, 1), lds(29, True, 1)
+    assert general - inv == (29 - 1) * (16 * 16 + 24 * 8) * 4       # As and M slots
+    assert lds(29, False, 1, coresident=True) - lds(29, True, 1, coresident=True) == general - inv
+    assert lds(29, True, 2) == lds(29, False, 2)                     # split: general path
+    assert lds(20, True, 1, stride=1, W=27) == lds(20, False, 1, stride=1, W=27)
+    assert fs.step_coresidency(128, 29, 128, 32, 8, 0, True, True) == 2
