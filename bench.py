@@ -675,7 +675,8 @@ def main(argv=None):
                        "input_batches_rotated": K, "pred_layout": args.pred_layout,
                        "targets_shared": shared,
                        "workgroups_per_scene": fs.step_split(S, F, H, Nmax, b.pos.shape[1], b.stride,
-                                                             args.split, cores),
+                                                             args.split, cores,
+                                                             targets_shared=shared),
                        "coresident": cores,
                        "workgroups_per_cu": fs.step_coresidency(S, F, H, Nmax, b.pos.shape[1], b.stride,
                                                                 cores, shared),

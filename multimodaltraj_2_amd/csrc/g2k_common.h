@@ -391,9 +391,19 @@ inline bool split_automatic(const g2k_dims& d) {
   return ((d.flags & G2K_STEP_SPLIT_MASK) >> G2K_STEP_SPLIT_SHIFT) == 0 &&
          !(d.flags & G2K_STEP_CORESIDENT);
 }
+// Every frame of a launch has the same inputs — stride 0 (each frame reads the
+// same window rows) and one target set for every frame — so one frame's work
+// stands for all (g2k_scene.hip frames_invariant).  The train kernels' form
+// of it also needs the L2 loss and dWo kept per worker (Nmax <= 85:
+// SceneLayout::dwo_seq == 0 at 12 gradient workers).
+inline bool frames_invariant_dims(const g2k_dims& d) {
+  return d.stride == 0 && (d.flags & G2K_STEP_TARGETS_SHARED) && !(d.flags & G2K_STEP_LOSS_NLL) &&
+         12 * d.Nmax * 8 * 4 <= 32 * 1024;
+}
 inline int scene_split_cus(const g2k_dims& d, int cus) {
   int x = (d.flags & G2K_STEP_SPLIT_MASK) >> G2K_STEP_SPLIT_SHIFT;
   if (x == 0 && (d.flags & G2K_STEP_CORESIDENT)) x = 1;   // launches in flight fill the CUs
+  if (x == 0 && frames_invariant_dims(d)) x = 1;          // one frame's work per chunk: nothing to share
   if (x == 0) x = d.S >= cus ? 1 : (d.S > 0 ? cus / d.S : 1);
   if (x > kMaxSplit) x = kMaxSplit;
   if (x > d.F) x = d.F;

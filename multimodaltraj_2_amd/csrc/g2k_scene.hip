@@ -143,12 +143,14 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
 // same window rows) and one target set for every frame
 // (G2K_STEP_TARGETS_SHARED) — sample.py's time-slice scenes, the train.py
 // legs.  E, A, As, cost, M, Y and the a9 terms are then the same in every
-// frame and only h changes along them, so the forward (g2k_scene_kernel<...,
-// INV>, one workgroup per scene) forms one head and one set of tiles per chunk
-// and replicates their outputs over the chunk's frames; its rings hold one
-// slot.
+// frame and only h changes along them, so the step (g2k_scene_kernel<...,
+// INV>, one workgroup per scene: the automatic split is 1) forms one head and
+// one set of tiles per chunk, replicates their outputs over the chunk's frames
+// and, in train mode, adds their gradient terms with weight n (the frames of
+// the chunk); its rings hold one slot.
 __host__ inline bool frames_invariant(const g2k_dims& d, bool grad) {
-  return !grad && d.stride == 0 && (d.flags & G2K_STEP_TARGETS_SHARED) && scene_split(d) == 1;
+  (void)grad;   // (train mode: frames_invariant_dims also excludes the NLL loss and dwo_seq)
+  return frames_invariant_dims(d) && scene_split(d) == 1;
 }
 
 __host__ inline SceneLayout scene_layout(const g2k_dims* d, int NP, bool grad) {
@@ -1096,10 +1098,12 @@ __device__ __forceinline__ f32x4 mm16(FA fa, FB fb, int L, int q) {
 //   dWc_f[r][u] = sum_t dM[r][t] cost[u][t]
 //   dK1_f[t][j] = sum_d dE[t][d] Uaug[j][d]        (E = K1 @ Uaug, j < 10)
 //   dUaug_f[j][d] = sum_t K1[t][j] dE[t][d]        (j < 8: window rows, 8-9: Ve, 10: bv)
-template <bool OPAQUE>
+// REP (frames_invariant): the frame stands for `wrep` frames with the same
+// terms; they enter the sums with that weight.
+template <bool OPAQUE, bool REP = false>
 __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout& lay,
                                            const SceneCtx& c, int fl, const f32x4 (&dm)[2],
-                                           int slot) {
+                                           int slot, float wrep = 1.f) {
   // The products chain through the MFMA registers: a result D (lane (L, q)
   // reg v = D[4q+v][L]) is the next product's B operand as is (k = 4q + ks
   // <-> reg ks) or its A operand transposed (A[L][4q+ks] = D[4q+ks][L]), so
@@ -1188,6 +1192,12 @@ __device__ __forceinline__ void frame_grad(const StepArgs& a, const SceneLayout&
     dK = mfma4(dET[ks], ua[ks], dK);
   }
   // into this producer's sums
+  if constexpr (REP) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      w0[v] *= wrep; w1[v] *= wrep; dK[v] *= wrep; dU[v] *= wrep;
+    }
+  }
   if (L < kT) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -1365,12 +1375,15 @@ __device__ __forceinline__ void balance_stores(const StepArgs& a) {
 // each tile loads the next tile's targets as soon as its own are consumed,
 // before its prediction stores (tg holds the first tile's targets on entry
 // when `preloaded`).
-template <bool PM, bool NLL>
+// REP (frames_invariant): frame f0 stands for the `nrep` frames fb .. fb +
+// nrep - 1 — its predictions are stored for each of them, its terms enter the
+// sums with weight nrep.
+template <bool PM, bool NLL, bool REP = false>
 __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int slot, int fb, int f0, int fstep,
                                             int fend, unsigned act_bits, float (&acc)[5],
                                             float& lsum, float2 (&tg)[4], bool preloaded,
-                                            int t0 = 0, int t1 = -1) {
+                                            int t0 = 0, int t1 = -1, int nrep = 1) {
   const int Nmax = a.d.Nmax, F = a.d.F, L = c.L, q = c.q;
   const int ntact = t1 < 0 ? c.ntact : t1;             // tiles [t0, ntact) of each frame
   const brsrc tgr = scene_targets_rsrc(a, c.s);
@@ -1384,16 +1397,22 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
     const int f = fb + fl;
     const int ford = f / lay.split;                      // the workgroup's own frames in order (dwo_seq)
     poll_flag(c.sMflag + fl, f + 1);                     // M of this frame (a producer's head)
-    const brsrc pr = make_brsrc(a.pred ? a.pred + ((size_t)c.s * F + f) * kL2 * Nmax : a.targets,
-                                a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
+    const brsrc pr = REP ? make_brsrc(a.pred ? a.pred + ((size_t)c.s * F + fb) * kL2 * Nmax : a.targets,
+                                      a.pred ? (uint32_t)(nrep * kL2 * Nmax * 4) : 0u)
+                         : make_brsrc(a.pred ? a.pred + ((size_t)c.s * F + f) * kL2 * Nmax : a.targets,
+                                      a.pred ? (uint32_t)kL2 * Nmax * 4 : 0u);
     for (int t = t0; t < ntact; ++t) {
       const bool nxt = t + 1 < ntact;                    // the next tile: this frame's, else the next frame's
       const int nfl = nxt ? fl : fl + fstep, nt = nxt ? t + 1 : t0;
       f32x4 dWoT;
-      pred_tile<true, PM, NLL>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u,
-                               Nmax, c.nact, t, L, q, acc, lsum, dm, dWoT,
-                               [&] { load_targets(tgr, Nmax, c.nact, fb, nfl, nt, nfl < fend, L, q, tg, lay.tfb); },
-                               c.sNllC, c.sNllA + slot * 12 * 64 + c.lane);
+      pred_tile<true, PM, NLL, REP>(c.sMring + fl * kL2 * kT, c.sWo, ys, pr, tg, (act_bits >> t) & 1u,
+                                    Nmax, c.nact, t, L, q, acc, lsum, dm, dWoT,
+                                    [&] { load_targets(tgr, Nmax, c.nact, fb, nfl, nt, nfl < fend, L, q, tg, lay.tfb); },
+                                    c.sNllC, c.sNllA + slot * 12 * 64 + c.lane, nrep);
+      if constexpr (REP) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) dWoT[v] *= (float)nrep;
+      }
       // dWo^T[n0 + 4q + v][t = L]: one copy per worker, or one copy added
       // to in frame order (tile sequence word) when that is too big
       const int nb = 16 * t + 4 * q;
@@ -1418,7 +1437,7 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
         if (q < 2) dMs[mrow(16 + 4 * q + v) * kT + L] = dm[1][v];
       }
     }
-    frame_grad<NLL>(a, lay, c, fl, dm, slot);
+    frame_grad<NLL, REP>(a, lay, c, fl, dm, slot, (float)nrep);
     dm[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     dm[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -1555,8 +1574,9 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // GRAD: this producer's own frames (ordinals) pw, pw + NP, ... < gend of
     // the chunk (the last R own frames of the last chunk go to the
     // recurrence waves)
-    const int R = GRAD && fb + lay.fc >= c.nf ? grad_rec_frames(own.n, NP) : 0;
-    const int gend = own.n - R;
+    // (INV: producer 0 takes the chunk's frame 0, standing for all cnt)
+    const int R = GRAD && !INV && fb + lay.fc >= c.nf ? grad_rec_frames(own.n, NP) : 0;
+    const int gend = INV ? (own.n < 1 ? own.n : 1) : own.n - R;
     // the first tiles' targets: in flight during the heads (GRAD: one buffer
     // and the balancing stores, see grad_frames)
     if (GRAD) {
@@ -1576,7 +1596,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // of the first chunk's frames 0 .. nrh - 1 themselves (M only here).
     const bool all_heads = a.h_in != nullptr && c.x == 0;
     const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : c.X,
-              nh = all_heads ? (INV ? (cnt < 1 ? cnt : 1) : cnt) : own.n;
+              nh = INV ? (cnt < 1 ? cnt : 1) : (all_heads ? cnt : own.n);   // (INV: one ring slot)
     const int nrep = INV ? cnt : 1;              // frames one head / tile stands for
     const int nrh = all_heads && fb == 0 ? rec_head_frames<CR, INV>(lay, c) : 0;
     for (int i = pw; i < nh; i += NP) {
@@ -1610,8 +1630,8 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // phase 2 — predictions and errors (GRAD: and the gradient)
     if (CR) __builtin_amdgcn_s_setprio(3);
     if (GRAD) {
-      grad_frames<PM, NLL>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
-                           act_bits, acc, lsum, tg[0], true);
+      grad_frames<PM, NLL, INV>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
+                                act_bits, acc, lsum, tg[0], true, 0, -1, INV ? cnt : 1);
       if (pw < R && grad_rec_tiles(ntact) < ntact) {    // the recurrence waves' frames' other tiles
         const int fl = own.fo + c.X * (gend + pw);
         grad_frames<PM, NLL>(a, lay, c, pw, fb, fl, 1, fl + 1, act_bits, acc, lsum, tg[0], false,
@@ -1787,7 +1807,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
 // GRAD, recurrence wave w after its recurrence: the last R frames of the
 // last chunk (frame cnt - R + w) as gradient worker NP + w, then its metrics
 // row and ticket (with zero partials when R = 0).
-template <int NP, bool PM, bool NLL>
+template <int NP, bool PM, bool NLL, bool INV>
 __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayout& lay,
                                               const SceneCtx& c) {
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1796,7 +1816,7 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
     const int fb = ((c.nf - 1) / lay.fc) * lay.fc;
     const int cnt = c.nf - fb;
     const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
-    const int R = grad_rec_frames(own.n, NP);
+    const int R = INV ? 0 : grad_rec_frames(own.n, NP);   // (INV: producer 0 has the one frame)
     if (R > 0) {
       float2 tg[4];
       grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, own.fo + c.X * (own.n - R + c.wv), c.X * R,
@@ -1931,7 +1951,7 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   if (c.wv < kRecW) {
     scalars();
     scene_recurrence<TPW, NP, CR, !GRAD, INV>(a, lay, c);
-    if (GRAD) rec_grad_work<NP, PM, NLL>(a, lay, c);
+    if (GRAD) rec_grad_work<NP, PM, NLL, INV>(a, lay, c);
   } else {
     scalars();
     scene_producer<NP, GRAD, PM, NLL, CR, INV>(a, lay, c);
@@ -1968,8 +1988,8 @@ void launch_kp(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
   const size_t lds = (size_t)l.total * 4;
   if (GRAD && loss_nll(a.d))
     hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, GRAD, false>), grid, block, lds, st, a, l);
-  else if (!GRAD && frames_invariant(a.d, false))
-    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, !GRAD>), grid, block, lds, st, a, l);
+  else if (frames_invariant(a.d, GRAD))   // stride 0, shared targets, one workgroup per scene
+    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, true>), grid, block, lds, st, a, l);
   else
     hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, false>), grid, block, lds, st, a, l);
 }

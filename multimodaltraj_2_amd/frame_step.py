@@ -166,35 +166,44 @@ def device_cus(device) -> int:
     return int(torch.cuda.get_device_properties(device).multi_processor_count)
 
 
-def split_for_cus(S, F, split=0, coresident=False, cus=256) -> int:
+def split_for_cus(S, F, split=0, coresident=False, cus=256, *, stride=1, targets_shared=False,
+                  Nmax=1, loss="l2") -> int:
     """Workgroups per scene for a device with ``cus`` CUs: the request, or the
     library's automatic choice (g2k_step_split_for_cus, ABI 9: host
-    arithmetic, no HIP call — the same answer with or without a GPU)."""
+    arithmetic, no HIP call — the same answer with or without a GPU).  The
+    choice is 1 for loop-invariant launches (stride 0 with shared targets:
+    one frame's work per chunk, g2k_scene.hip frames_invariant), so the
+    stride, the targets' sharing, Nmax and the loss take part."""
     lib = _lib.load()
-    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 128, 1, max(F, 1) + OBS_LEN, 1,
-                     step_flags(split=split, coresident=coresident))
+    W = (max(F, 1) - 1) * stride + OBS_LEN
+    d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 128, max(int(Nmax), 1), W, stride,
+                     step_flags(targets_shared=targets_shared, loss=loss, split=split,
+                                coresident=coresident))
     x = int(lib.g2k_step_split_for_cus(ctypes.byref(d), int(cus)))
     if x < 1:
         _lib.check("g2k_step_split_for_cus", -1)
     return x
 
 
-def plan_split(S, F, split, coresident, device) -> int:
+def plan_split(S, F, split, coresident, device, **kw) -> int:
     """The explicit split a plan launches with: an automatic request (0) is
     resolved HERE for the plan's own device and passed to the library as
     G2K_STEP_SPLIT(x), so sizing and launch never depend on which device is
     current (include/g2k_hip.h); 0 stays 0 under G2K_STEP_CORESIDENT (the
-    library's 1)."""
+    library's 1).  ``kw``: split_for_cus's stride / targets_shared / Nmax /
+    loss."""
     if split or coresident:
         return split
-    return split_for_cus(S, F, 0, False, device_cus(device))
+    return split_for_cus(S, F, 0, False, device_cus(device), **kw)
 
 
-def step_split(S, F, H, Nmax, W, stride, split=0, coresident=False, device=None) -> int:
+def step_split(S, F, H, Nmax, W, stride, split=0, coresident=False, device=None,
+               targets_shared=False) -> int:
     """Workgroups per scene a plan on ``device`` (default: the current one)
     uses: the request, or the automatic choice for that device's CUs."""
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    return split_for_cus(S, F, split, coresident, device_cus(dev))
+    return split_for_cus(S, F, split, coresident, device_cus(dev), stride=stride,
+                         targets_shared=targets_shared, Nmax=Nmax)
 
 
 def step_workspace_bytes(S, F, H, Nmax, W, stride) -> int:
@@ -276,7 +285,8 @@ def _prepare_step(params, pos, vislet, G, targets, n_active, h, n_frames, ped_ma
     if two != 2:
         raise ValueError(f"pos: last dim {two}, expected 2")
     F = step_frames(targets, targets_shared, frames)
-    split = plan_split(S, F, split, coresident, dev)
+    split = plan_split(S, F, split, coresident, dev, stride=stride, targets_shared=targets_shared,
+                       Nmax=Nmax)
     flags = step_flags(pred_layout, targets_shared, split=split, coresident=coresident)
     H = int(h.shape[2])
     params.check(dev)

@@ -91,7 +91,8 @@ class GradPlan:
             _check_dev("ped_mask", ped_mask, dev, torch.uint8)
         if loss == "nll" and params.head is None:
             raise ValueError('loss "nll" needs params.head [3, 12]')
-        split = plan_split(S, F, split, False, dev)       # explicit: device-independent sizes
+        split = plan_split(S, F, split, False, dev, stride=stride, targets_shared=targets_shared,
+                           Nmax=Nmax, loss=loss)       # explicit: device-independent sizes
         d = _lib.G2KDims(S, F, OBS_LEN, PRED_LEN, HIDDEN_LEN, 64, Nmax, W, stride,
                          step_flags("band", targets_shared, loss, split))
         P = int(lib.g2k_grad_size(ctypes.byref(d)))
@@ -162,7 +163,8 @@ class TrainPlan:
             raise ValueError('loss "nll" needs params.head [3, 12]')
         # one explicit split for the forward plan and the train launch alike
         split = plan_split(int(pos.shape[0]), step_frames(targets, targets_shared, frames), split,
-                           False, pos.device)
+                           False, pos.device, stride=stride, targets_shared=targets_shared,
+                           Nmax=int(pos.shape[2]), loss=loss)
         self.fwd = StepPlan(params, pos, vislet, G, targets, n_active, h, n_frames=n_frames,
                             ped_mask=ped_mask, stride=stride, lam=lam, out=out, stream=stream,
                             pred_layout=pred_layout, targets_shared=targets_shared, frames=frames,

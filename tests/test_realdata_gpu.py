@@ -70,13 +70,19 @@ def test_every_real_scene_matches_oracle(gpu, plan, dev_batch, shared):
         assert close(met[s, :6], m[:6]) <= TOL, s
 
 
-def test_real_launch_gradient_matches_oracle(gpu, plan, dev_batch):
+@pytest.mark.parametrize("shared", [False, True])
+def test_real_launch_gradient_matches_oracle(gpu, plan, dev_batch, shared):
+    """shared: one target set per scene — the automatic split is 1 and the
+    gradient takes the loop-invariant train path (one frame's terms with
+    weight n_frames, g2k_scene.hip frames_invariant)."""
     S = 32
     Nmax = plan.Nmax
     params = fs.init_params(Nmax, seed=0, device=gpu)
     t = {k: (v[:S] if isinstance(v, torch.Tensor) else v) for k, v in dev_batch.items()}
-    gp = ts.GradPlan(params, t["pos"], t["vislet"], t["G"], t["targets"], t["n_active"],
-                     n_frames=t["n_frames"], ped_mask=t["ped_mask"], stride=0)
+    tgt = t["targets"][:, :1].contiguous() if shared else t["targets"]
+    gp = ts.GradPlan(params, t["pos"], t["vislet"], t["G"], tgt, t["n_active"],
+                     n_frames=t["n_frames"], ped_mask=t["ped_mask"], stride=0,
+                     targets_shared=shared, frames=int(t["targets"].shape[1]) if shared else None)
     g = gp.run().double().cpu().numpy()
     h = plan.host()
     G = dev_batch["G"].cpu().numpy()
