@@ -88,7 +88,13 @@ typedef struct g2k_dims {
  * automatic (x = min(4, CUs / S) for the current device's CU count — 256 on
  * MI355X, 256 assumed without a device — at most F: a launch of fewer scenes
  * than the device has CUs spreads each scene's frames over x workgroups, the
- * first of which also runs the recurrence; g2k_step_split reports x).  x > 1
+ * first of which also runs the recurrence; g2k_step_split reports x).  The
+ * automatic choice is 1 for loop-invariant launches — stride 0 with
+ * G2K_STEP_TARGETS_SHARED (and, for the automatic rule, the L2 loss and
+ * Nmax <= 85): every frame has the same inputs, and with one workgroup per
+ * scene the step forms one frame's head, tiles and gradient terms per chunk
+ * and replicates / weights them (pred, h, attn, cost as the general path's;
+ * metric sums and gradients n_frames x one frame's).  x > 1
  * needs the workspace (g2k_step_workspace_bytes / g2k_train_workspace_bytes /
  * g2k_grad_workspace_bytes); its contents need no initialisation: every launch
  * zeroes the scene tickets in it on its own stream first (a memset ahead of
