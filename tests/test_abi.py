@@ -220,6 +220,14 @@ def test_split_sizing_without_a_gpu_is_explicit():
     assert fs.split_for_cus(100, 20, cus=80) == 1
     assert fs.split_for_cus(128, 20, split=3, cus=256) == 3          # the request
     assert fs.split_for_cus(128, 20, coresident=True, cus=256) == 1  # launches in flight
+    # loop-invariant launches (stride 0, shared targets; L2, Nmax <= 85): one frame's work
+    inv = dict(stride=0, targets_shared=True, Nmax=32)
+    assert fs.split_for_cus(128, 20, cus=256, **inv) == 1
+    assert fs.split_for_cus(128, 20, split=2, cus=256, **inv) == 2          # the request stands
+    assert fs.split_for_cus(128, 20, cus=256, stride=0, targets_shared=False, Nmax=32) == 2
+    assert fs.split_for_cus(128, 20, cus=256, stride=1, targets_shared=True, Nmax=32) == 2
+    assert fs.split_for_cus(128, 20, cus=256, stride=0, targets_shared=True, Nmax=128) == 2
+    assert fs.split_for_cus(128, 20, cus=256, loss="nll", **inv) == 2
     d = _lib.G2KDims(128, 20, 8, 12, 16, 128, 32, 27, 1, 0)
     assert lib.g2k_step_split_for_cus(ctypes.byref(d), 0) == -1
     sizes = set()
