@@ -112,8 +112,8 @@ PROLOGUE = [
      "    G2K_TL(60, c.wv == 0);\n"),
     ("    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)",
      "    G2K_TL(61, c.wv == 0);\n    if (c.tid < lay.fc) {                                // flags hold (global frame + 1)"),
-    ("    scalars();\n    scene_recurrence<TPW, NP, CR>(a, lay, c);",
-     "    scalars();\n    G2K_TL(62, c.wv == 0);\n    scene_recurrence<TPW, NP, CR>(a, lay, c);"),
+    ("    scalars();\n    scene_recurrence<TPW, NP, CR, !GRAD, INV>(a, lay, c);",
+     "    scalars();\n    G2K_TL(62, c.wv == 0);\n    scene_recurrence<TPW, NP, CR, !GRAD, INV>(a, lay, c);"),
     ("  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)\n",
      "  __builtin_amdgcn_s_waitcnt(0x0070);                           // vmcnt(0) lgkmcnt(0)\n"
      "  G2K_TL(63, (c.wv == 0 || c.wv == kRecW) && fb == 0);\n"),
@@ -174,6 +174,20 @@ GRADF = [
 ]
 if os.environ.get("TL_GRAD"):
     REPS += GRADF
+# TL_VTILE=1 (build): producer 0's first V tile (window rows 0..15), four stamps
+# (entry, after the k-loop's MFMAs, after the VG MFMAs, after the stores)
+VTILE = [
+    ("  const int nks = ((nact + 15) / 16) * 4;\n  f32x4 v0 =",
+     "  G2K_TL(122, w0 == 0);\n  const int nks = ((nact + 15) / 16) * 4;\n  f32x4 v0 ="),
+    ("  f32x4 vt;\n#pragma unroll\n  for (int i = 0; i < 4; ++i) vt[i] = v0[i] + v1[i];\n",
+     "  f32x4 vt;\n#pragma unroll\n  for (int i = 0; i < 4; ++i) vt[i] = v0[i] + v1[i];\n"
+     "  asm volatile(\"\" :: \"v\"(vt[0]), \"v\"(vt[3]));\n  G2K_TL(123, w0 == 0);\n"),
+    ("  const int row = win ? r : lay.wcmax + (r - wcc);               // storage row\n",
+     "  asm volatile(\"\" :: \"v\"(vg[0]), \"v\"(vg[3]));\n  G2K_TL(124, w0 == 0);\n"
+     "  const int row = win ? r : lay.wcmax + (r - wcc);               // storage row\n"),
+]
+if os.environ.get("TL_VTILE"):
+    REPS += VTILE
 FINE = {48: "heads loop entry", 49: "head 1", 50: "head 2", 51: "head 3", 52: "head 4", 53: "head 5", 54: "head 6", 55: "head 7+"}
 
 
@@ -226,7 +240,7 @@ def run(config, nstreams, split=0, cores=False):
     base = b.to_device(dev)
     params = fs.init_params(Nmax, seed=0).to(dev)
     streams = [torch.cuda.Stream(device=dev) for _ in range(nstreams)]
-    K = 3 * nstreams
+    K = min(3 * nstreams, 8192 // S)   # (the stamp buffer holds 8192 workgroups)
     plans = []
     for k in range(K):
         t = {key: (v.clone() if isinstance(v, torch.Tensor) else v) for key, v in base.items()}
@@ -323,6 +337,10 @@ def run(config, nstreams, split=0, cores=False):
         print(f"warm test: vtile0 first {d(112, 113):.0f} second {d(113, 114):.0f}; "
               f"vtile1 first {d(115, 116):.0f} second {d(116, 117):.0f}; "
               f"kmats first {d(118, 119):.0f} second {d(119, 120):.0f}")
+    if np.any(r[:, 124] != 0):
+        d = lambda i, j: np.median(((r[:, j] - r[:, i]) % (1 << 32))[(r[:, j] != 0) & (r[:, i] != 0)])   # noqa: E731
+        print(f"vtile 0: entry at {np.median((rel(122) - start)[r[:, 122] != 0]):.0f}, k-loop {d(122, 123):.0f}, "
+              f"VG {d(123, 124):.0f}, to staged {d(124, 59):.0f}")
     print("lead (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in st.items()))
     pro = {"start - entry": (r[:, 4] - r[:, 70]) % (1 << 32), "pos dma issued": rel(60) - start, "segments issued": rel(61) - start,
            "rec0 scalars": rel(62) - start, "loads landed (w0 or p0)": rel(63) - start}
