@@ -665,7 +665,7 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
   if (c.wv >= kRecW) {
     const int ntile = (wcc + 3 + 15) / 16;
     const int ntask = ntile + (fb == 0 ? (PAD ? 2 : 1) : 0);
-    for (int task = c.wv - kRecW; task < ntask; task += NP) {
+    auto run = [&](int task) {
       if (task < ntile) {
         scene_vtile<PAD>(a, lay, c, 16 * task, wcc);
       } else if (!PAD || task == ntile) {
@@ -674,7 +674,17 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
       } else {
         if constexpr (PAD) scene_pad_consts(c, lay, a.lambda);
       }
+    };
+    // forward (PAD): the first task outside the loop — a loop's preheader
+    // would form every task kind's addresses (and reload spilled scalars)
+    // after B1, ahead of the first task, on the lead's critical path
+    int task = c.wv - kRecW;
+    if (PAD && task < ntask) {
+      run(task);
+      task += NP;
     }
+#pragma unroll 1
+    for (; task < ntask; task += NP) run(task);
   } else {
     rec_init();
   }
