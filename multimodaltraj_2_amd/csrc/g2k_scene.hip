@@ -86,6 +86,8 @@ struct SceneLayout {
   int tfb;             // target bytes per frame (0: one set for every frame, G2K_STEP_TARGETS_SHARED)
   int split;           // workgroups per scene (scene_split): workgroup x owns the frames g = x mod split
   int total;           // floats
+  int own0;            // > 0 (train, split 2): block ownership instead — workgroup 0 owns the first
+                       // min(own0, cnt / 2) frames of each chunk, workgroup 1 the rest (own_frames)
 };
 
 __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int F, int fc, int NP,
@@ -93,6 +95,7 @@ __host__ __device__ inline SceneLayout scene_layout_fc(int Nmax, int stride, int
   SceneLayout s;
   s.fc = fc;
   s.split = 1;
+  s.own0 = 0;
   s.tfb = Nmax * kL2 * 4;
   s.wcmax = (fc - 1) * stride + kT;
   s.pp = 2 * Nmax;                            // unpadded: the chunk's rows are one contiguous copy
@@ -164,18 +167,40 @@ __host__ inline SceneLayout scene_layout(const g2k_dims* d, int NP, bool grad) {
   }
   l.tfb = (d->flags & G2K_STEP_TARGETS_SHARED) ? 0 : d->Nmax * kL2 * 4;
   l.split = scene_split(*d);
+  // train mode, two workgroups per scene: workgroup 0 also forms every frame's
+  // As head for the chain (and runs the chain on its SIMDs), so it owns fewer
+  // frames (M, tiles, gradient) than workgroup 1 — the modular split left it
+  // ~10k cycles behind (kfold4 train, profiles/r12j_*).  One frame per
+  // producer measured best: kfold4 train 41.1 -> 38.6 us per step at 8 of 20
+  // frames, 42.0-42.2 at 7 or 9 (profiles/r12kl_*)
+  if (grad && l.split == 2 && !l.dwo_seq) l.own0 = NP;
   return l;
 }
 
 // The frames of chunk [fb, fb + cnt) a workgroup owns (global frames g with
-// g mod split == x): local frames fo + split * i, i < n.
+// g mod split == x): local frames fo + split * i, i < n.  own0 > 0
+// (SceneLayout::own0, split 2, the BLK kernels): blocks — workgroup 0 the
+// chunk's first n0 frames, workgroup 1 the rest (local frames fo + i).
 struct OwnFrames {
   int fo, n;
 };
-__device__ __forceinline__ OwnFrames own_frames(int fb, int cnt, int split, int x) {
+__device__ __forceinline__ int own_block0(int cnt, int own0) {
+  const int h = cnt / 2;
+  return own0 < h ? own0 : h;
+}
+__device__ __forceinline__ OwnFrames own_frames(int fb, int cnt, int split, int x, int own0) {
+  if (own0 > 0) {
+    const int n0 = own_block0(cnt, own0);
+    return x == 0 ? OwnFrames{0, n0} : OwnFrames{n0, cnt - n0};
+  }
   int fo = x - fb % split;
   if (fo < 0) fo += split;
   return OwnFrames{fo, fo < cnt ? (cnt - fo + split - 1) / split : 0};
+}
+// the workgroup owning local frame fl of chunk [fb, fb + cnt)
+__device__ __forceinline__ int frame_owner(int fb, int cnt, int fl, int split, int own0) {
+  if (own0 > 0) return fl < own_block0(cnt, own0) ? 0 : 1;
+  return (fb + fl) % split;
 }
 
 // frame head output: the x / y row tiles of M^T
@@ -698,7 +723,7 @@ __device__ __forceinline__ void scene_stage(const StepArgs& a, const SceneLayout
 // HBM burst, which every wave's B1 waits for, stays free of it) and its
 // softmax numerators are formed there too; after B2 the waves form As of the
 // first frames themselves and start the chain.
-template <int TPW, int NP, bool CR, bool PAD, bool INV>
+template <int TPW, int NP, bool CR, bool PAD, bool INV, bool BLK = false>
 __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneLayout& lay,
                                                  const SceneCtx& c) {
   constexpr int NT = 64 * (kRecW + NP);
@@ -733,7 +758,7 @@ __device__ __forceinline__ void scene_recurrence(const StepArgs& a, const SceneL
     __builtin_amdgcn_s_setprio(3);
     float rm[4];
     scene_rm(lay, c, rm);
-    const bool mine = c.X == 1 || fl % c.X == 0;
+    const bool mine = c.X == 1 || (BLK ? frame_owner(0, c.nf < lay.fc ? c.nf : lay.fc, fl, c.X, lay.own0) : fl % c.X) == 0;
     // the co-resident geometry: these frames' M too (its producers skip
     // them).  Not in train mode: there the producers form these frames' M
     // AND the cost their gradient terms read (sCost), and the M flag must not
@@ -1327,13 +1352,22 @@ __device__ __forceinline__ unsigned scene_act_bits(const SceneCtx& c, uint32_t w
 // Train mode: the last R frames of the scene's last chunk go to the
 // recurrence waves (one each, after their recurrence), so the producers'
 // share shrinks when they have at least two frames each.
-__device__ __forceinline__ int grad_rec_frames(int cnt, int NP) { return cnt >= 2 * NP ? kRecW : 0; }
+__device__ __forceinline__ int grad_rec_frames(int cnt, int NP, bool live) {
+  // a workgroup without the chain (a split scene's other workgroups): its
+  // recurrence waves are free from the start — whole frames, one each, once
+  // the producers keep one each
+  if (!live) return cnt >= NP + kRecW ? kRecW : 0;
+  return cnt >= 2 * NP ? kRecW : 0;
+}
 // ... split by tile when a frame has two or more: the recurrence wave takes
 // tiles [0, h) (it starts at the chain's end), producer w (w < R, free after
 // its own frames; the last R producers measured slower) tiles [h, ntact) of
 // the same frame; each adds its partial
 // dM's weight-side terms (frame_grad is linear in dM) into its own sums
-__device__ __forceinline__ int grad_rec_tiles(int ntact) { return ntact >= 2 ? (ntact + 1) / 2 : ntact; }
+__device__ __forceinline__ int grad_rec_tiles(int ntact, bool live) {
+  if (!live) return ntact;
+  return ntact >= 2 ? (ntact + 1) / 2 : ntact;
+}
 
 // The targets of tile t of chunk frame fl in pred_tile's order (pedestrian
 // 16 t + L, floats 4q .. 4q + 3 and 16 + 4q .. 16 + 4q + 3 of its row, zero
@@ -1529,7 +1563,7 @@ __device__ __forceinline__ void publish_metrics(const StepArgs& a, const SceneCt
 }
 
 // Role 2: the producers (waves 4..4+NP-1).
-template <int NP, bool GRAD, bool PM, bool NLL, bool CR, bool INV>
+template <int NP, bool GRAD, bool PM, bool NLL, bool CR, bool INV, bool BLK = false>
 __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLayout& lay,
                                                const SceneCtx& c) {
   const int Nmax = a.d.Nmax, F = a.d.F, stride = a.d.stride;
@@ -1544,11 +1578,12 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
   // (local frame ofo + X i for own-frame ordinal i = j / ntact).
   const uint32_t inv = 65536u / (uint32_t)(ntact > 0 ? ntact : 1) + 1u;
   int ofo = 0;
+  const int own0 = BLK ? lay.own0 : 0;   // (block ownership: BLK builds only)
   auto item_ft = [&](int k, int& fl, int& t) {
     const int j = pw + k * NP;
     const int i = (int)(((uint32_t)j * inv) >> 16);
     t = j - i * ntact;
-    fl = ofo + c.X * i;
+    fl = ofo + (BLK ? 1 : c.X) * i;
   };
   const brsrc tgr = scene_targets_rsrc(a, s);
   // forward target buffers in flight per producer (4 with 4 producers
@@ -1577,20 +1612,22 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
       scene_stage<64 * (kRecW + NP), NP, !GRAD, NLL>(a, lay, c, fb, cnt, [] {});
     }
     if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
-    const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
+    const OwnFrames own = own_frames(fb, cnt, c.X, c.x, own0);
     ofo = own.fo;
+    const int ostep = BLK ? 1 : c.X;        // own frames' local stride (BLK: blocks)
     const int nown = INV ? (own.n < 1 ? own.n : 1) : own.n;   // (INV: frame 0 only)
     const int nitems = nown * ntact > pw ? (nown * ntact - pw + NP - 1) / NP : 0;   // forward
     // GRAD: this producer's own frames (ordinals) pw, pw + NP, ... < gend of
     // the chunk (the last R own frames of the last chunk go to the
     // recurrence waves)
     // (INV: producer 0 takes the chunk's frame 0, standing for all cnt)
-    const int R = GRAD && !INV && fb + lay.fc >= c.nf ? grad_rec_frames(own.n, NP) : 0;
+    const bool live = !BLK || (a.h_in != nullptr && c.x == 0);   // (BLK: does this workgroup run the chain?)
+    const int R = GRAD && !INV && fb + lay.fc >= c.nf ? grad_rec_frames(own.n, NP, live) : 0;
     const int gend = INV ? (own.n < 1 ? own.n : 1) : own.n - R;
     // the first tiles' targets: in flight during the heads (GRAD: one buffer
     // and the balancing stores, see grad_frames)
     if (GRAD) {
-      load_targets(tgr, Nmax, c.nact, fb, own.fo + c.X * pw, 0, pw < gend, L, q, tg[0], lay.tfb);
+      load_targets(tgr, Nmax, c.nact, fb, own.fo + ostep * pw, 0, pw < gend, L, q, tg[0], lay.tfb);
       balance_stores<PM>(a);
     } else {
 #pragma unroll
@@ -1605,14 +1642,14 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // (and A / cost out) only for own frames.  The recurrence waves form As
     // of the first chunk's frames 0 .. nrh - 1 themselves (M only here).
     const bool all_heads = a.h_in != nullptr && c.x == 0;
-    const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : c.X,
+    const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : ostep,
               nh = INV ? (cnt < 1 ? cnt : 1) : (all_heads ? cnt : own.n);   // (INV: one ring slot)
     const int nrep = INV ? cnt : 1;              // frames one head / tile stands for
     const int nrh = all_heads && fb == 0 ? rec_head_frames<CR, INV>(lay, c) : 0;
     for (int i = pw; i < nh; i += NP) {
       const int fl = hb + hs * i;
       const int f = fb + fl;
-      const bool mine = !all_heads || c.X == 1 || f % c.X == c.x;
+      const bool mine = !all_heads || c.X == 1 || (BLK ? frame_owner(fb, cnt, fl, c.X, own0) : f % c.X) == c.x;
       if (fl < nrh && (!mine || CR)) continue;   // (a recurrence wave formed As, and M under CR)
       // issue priority: the co-resident geometry is producer-bound, so its
       // producers outrank the chain (2 heads, 3 tiles; round 4,
@@ -1640,12 +1677,12 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // phase 2 — predictions and errors (GRAD: and the gradient)
     if (CR) __builtin_amdgcn_s_setprio(3);
     if (GRAD) {
-      grad_frames<PM, NLL, INV>(a, lay, c, pw, fb, own.fo + c.X * pw, c.X * NP, own.fo + c.X * gend,
+      grad_frames<PM, NLL, INV>(a, lay, c, pw, fb, own.fo + ostep * pw, ostep * NP, own.fo + ostep * gend,
                                 act_bits, acc, lsum, tg[0], true, 0, -1, INV ? cnt : 1);
-      if (pw < R && grad_rec_tiles(ntact) < ntact) {    // the recurrence waves' frames' other tiles
-        const int fl = own.fo + c.X * (gend + pw);
+      if (pw < R && grad_rec_tiles(ntact, live) < ntact) {    // the recurrence waves' frames' other tiles
+        const int fl = own.fo + ostep * (gend + pw);
         grad_frames<PM, NLL>(a, lay, c, pw, fb, fl, 1, fl + 1, act_bits, acc, lsum, tg[0], false,
-                             grad_rec_tiles(ntact), ntact);
+                             grad_rec_tiles(ntact, live), ntact);
       }
       // every worker done with the chunk's frames -> its dU rows into dV
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1817,7 +1854,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
 // GRAD, recurrence wave w after its recurrence: the last R frames of the
 // last chunk (frame cnt - R + w) as gradient worker NP + w, then its metrics
 // row and ticket (with zero partials when R = 0).
-template <int NP, bool PM, bool NLL, bool INV>
+template <int NP, bool PM, bool NLL, bool INV, bool BLK = false>
 __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayout& lay,
                                               const SceneCtx& c) {
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1825,14 +1862,16 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
   if (c.nf > 0) {
     const int fb = ((c.nf - 1) / lay.fc) * lay.fc;
     const int cnt = c.nf - fb;
-    const OwnFrames own = own_frames(fb, cnt, c.X, c.x);
-    const int R = INV ? 0 : grad_rec_frames(own.n, NP);   // (INV: producer 0 has the one frame)
+    const OwnFrames own = own_frames(fb, cnt, c.X, c.x, BLK ? lay.own0 : 0);
+    const bool live = !BLK || (a.h_in != nullptr && c.x == 0);
+    const int R = INV ? 0 : grad_rec_frames(own.n, NP, live);   // (INV: producer 0 has the one frame)
     if (R > 0) {
       float2 tg[4];
-      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, own.fo + c.X * (own.n - R + c.wv), c.X * R,
-                           own.fo + c.X * own.n,
+      const int ostep = BLK ? 1 : c.X;
+      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, own.fo + ostep * (own.n - R + c.wv), ostep * R,
+                           own.fo + ostep * own.n,
                            scene_act_bits(c, scene_mask_word(a, lay, c)),
-                           acc, lsum, tg, false, 0, grad_rec_tiles(c.ntact));
+                           acc, lsum, tg, false, 0, grad_rec_tiles(c.ntact, live));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (c.lane == 0) atomicAdd(c.sGseq, 1);
     }
@@ -1848,7 +1887,7 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
 template <int TPW, int NP>
 constexpr int scene_waves_per_eu() { return NP == 4 && TPW < 8 ? 4 : 1; }
 
-template <int TPW, int NP, bool GRAD, bool PM, bool NLL, bool INV>
+template <int TPW, int NP, bool GRAD, bool PM, bool NLL, bool INV, bool BLK = false>
 __global__ void __launch_bounds__(64 * (kRecW + NP))
 __attribute__((amdgpu_waves_per_eu(scene_waves_per_eu<TPW, NP>())))
 g2k_scene_kernel(StepArgs a, SceneLayout lay) {
@@ -1960,11 +1999,11 @@ g2k_scene_kernel(StepArgs a, SceneLayout lay) {
   };
   if (c.wv < kRecW) {
     scalars();
-    scene_recurrence<TPW, NP, CR, !GRAD, INV>(a, lay, c);
-    if (GRAD) rec_grad_work<NP, PM, NLL, INV>(a, lay, c);
+    scene_recurrence<TPW, NP, CR, !GRAD, INV, BLK>(a, lay, c);
+    if (GRAD) rec_grad_work<NP, PM, NLL, INV, BLK>(a, lay, c);
   } else {
     scalars();
-    scene_producer<NP, GRAD, PM, NLL, CR, INV>(a, lay, c);
+    scene_producer<NP, GRAD, PM, NLL, CR, INV, BLK>(a, lay, c);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
 }
@@ -2000,6 +2039,8 @@ void launch_kp(const StepArgs& a, const SceneLayout& l, hipStream_t st) {
     hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, GRAD, false>), grid, block, lds, st, a, l);
   else if (frames_invariant(a.d, GRAD))   // stride 0, shared targets, one workgroup per scene
     hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, true>), grid, block, lds, st, a, l);
+  else if (GRAD && l.own0 > 0)           // train, two workgroups per scene: block ownership
+    hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, false, GRAD>), grid, block, lds, st, a, l);
   else
     hipLaunchKernelGGL((g2k_scene_kernel<TPW, NP, GRAD, PM, false, false>), grid, block, lds, st, a, l);
 }

@@ -188,6 +188,18 @@ VTILE = [
 ]
 if os.environ.get("TL_VTILE"):
     REPS += VTILE
+# TL_DWI=1 (build, train): producer 0's dWi tile run twice, stamped before /
+# between / after (is the finalize's time the code's first fetch?)
+DWI = [
+    ("    if (n0 < c.nact) {\n      if (lay.fc >= F) dwi(c.sPos, lay.pp);\n      else dwi(a.pos + (size_t)c.s * a.d.W * Nmax * 2, 2 * Nmax);\n    }\n",
+     "    G2K_TL(108, pw == 0 && t == 0);\n"
+     "    if (n0 < c.nact) {\n      if (lay.fc >= F) dwi(c.sPos, lay.pp);\n      else dwi(a.pos + (size_t)c.s * a.d.W * Nmax * 2, 2 * Nmax);\n    }\n"
+     "    asm volatile(\"\" :: \"v\"(acc4[0]));\n    G2K_TL(109, pw == 0 && t == 0);\n    acc4 = f32x4{0.f, 0.f, 0.f, 0.f};\n"
+     "    if (n0 < c.nact) {\n      if (lay.fc >= F) dwi(c.sPos, lay.pp);\n      else dwi(a.pos + (size_t)c.s * a.d.W * Nmax * 2, 2 * Nmax);\n    }\n"
+     "    asm volatile(\"\" :: \"v\"(acc4[0]));\n    G2K_TL(110, pw == 0 && t == 0);\n"),
+]
+if os.environ.get("TL_DWI"):
+    REPS += DWI
 FINE = {48: "heads loop entry", 49: "head 1", 50: "head 2", 51: "head 3", 52: "head 4", 53: "head 5", 54: "head 6", 55: "head 7+"}
 
 
@@ -341,6 +353,9 @@ def run(config, nstreams, split=0, cores=False):
         d = lambda i, j: np.median(((r[:, j] - r[:, i]) % (1 << 32))[(r[:, j] != 0) & (r[:, i] != 0)])   # noqa: E731
         print(f"vtile 0: entry at {np.median((rel(122) - start)[r[:, 122] != 0]):.0f}, k-loop {d(122, 123):.0f}, "
               f"VG {d(123, 124):.0f}, to staged {d(124, 59):.0f}")
+    if np.any(r[:, 110] != 0):
+        d = lambda i, j: np.median(((r[:, j] - r[:, i]) % (1 << 32))[(r[:, j] != 0) & (r[:, i] != 0)])   # noqa: E731
+        print(f"dWi tile (producer 0): first run {d(108, 109):.0f}, second run {d(109, 110):.0f}")
     print("lead (cycles after start, medians):", "  ".join(f"{k} {np.median(v):.0f}" for k, v in st.items()))
     pro = {"start - entry": (r[:, 4] - r[:, 70]) % (1 << 32), "pos dma issued": rel(60) - start, "segments issued": rel(61) - start,
            "rec0 scalars": rel(62) - start, "loads landed (w0 or p0)": rel(63) - start}
