@@ -1614,7 +1614,6 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     if (fb == 0) act_bits = scene_act_bits(c, scene_mask_word(a, lay, c));   // (the row is in LDS)
     const OwnFrames own = own_frames(fb, cnt, c.X, c.x, own0);
     ofo = own.fo;
-    const int ostep = BLK ? 1 : c.X;        // own frames' local stride (BLK: blocks)
     const int nown = INV ? (own.n < 1 ? own.n : 1) : own.n;   // (INV: frame 0 only)
     const int nitems = nown * ntact > pw ? (nown * ntact - pw + NP - 1) / NP : 0;   // forward
     // GRAD: this producer's own frames (ordinals) pw, pw + NP, ... < gend of
@@ -1627,7 +1626,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // the first tiles' targets: in flight during the heads (GRAD: one buffer
     // and the balancing stores, see grad_frames)
     if (GRAD) {
-      load_targets(tgr, Nmax, c.nact, fb, own.fo + ostep * pw, 0, pw < gend, L, q, tg[0], lay.tfb);
+      load_targets(tgr, Nmax, c.nact, fb, own.fo + (BLK ? 1 : c.X) * pw, 0, pw < gend, L, q, tg[0], lay.tfb);
       balance_stores<PM>(a);
     } else {
 #pragma unroll
@@ -1642,7 +1641,7 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // (and A / cost out) only for own frames.  The recurrence waves form As
     // of the first chunk's frames 0 .. nrh - 1 themselves (M only here).
     const bool all_heads = a.h_in != nullptr && c.x == 0;
-    const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : ostep,
+    const int hb = all_heads ? 0 : own.fo, hs = all_heads ? 1 : (BLK ? 1 : c.X),
               nh = INV ? (cnt < 1 ? cnt : 1) : (all_heads ? cnt : own.n);   // (INV: one ring slot)
     const int nrep = INV ? cnt : 1;              // frames one head / tile stands for
     const int nrh = all_heads && fb == 0 ? rec_head_frames<CR, INV>(lay, c) : 0;
@@ -1677,10 +1676,10 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // phase 2 — predictions and errors (GRAD: and the gradient)
     if (CR) __builtin_amdgcn_s_setprio(3);
     if (GRAD) {
-      grad_frames<PM, NLL, INV>(a, lay, c, pw, fb, own.fo + ostep * pw, ostep * NP, own.fo + ostep * gend,
+      grad_frames<PM, NLL, INV>(a, lay, c, pw, fb, own.fo + (BLK ? 1 : c.X) * pw, (BLK ? 1 : c.X) * NP, own.fo + (BLK ? 1 : c.X) * gend,
                                 act_bits, acc, lsum, tg[0], true, 0, -1, INV ? cnt : 1);
       if (pw < R && grad_rec_tiles(ntact, live) < ntact) {    // the recurrence waves' frames' other tiles
-        const int fl = own.fo + ostep * (gend + pw);
+        const int fl = own.fo + (BLK ? 1 : c.X) * (gend + pw);
         grad_frames<PM, NLL>(a, lay, c, pw, fb, fl, 1, fl + 1, act_bits, acc, lsum, tg[0], false,
                              grad_rec_tiles(ntact, live), ntact);
       }
@@ -1867,9 +1866,8 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
     const int R = INV ? 0 : grad_rec_frames(own.n, NP, live);   // (INV: producer 0 has the one frame)
     if (R > 0) {
       float2 tg[4];
-      const int ostep = BLK ? 1 : c.X;
-      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, own.fo + ostep * (own.n - R + c.wv), ostep * R,
-                           own.fo + ostep * own.n,
+      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, own.fo + (BLK ? 1 : c.X) * (own.n - R + c.wv), (BLK ? 1 : c.X) * R,
+                           own.fo + (BLK ? 1 : c.X) * own.n,
                            scene_act_bits(c, scene_mask_word(a, lay, c)),
                            acc, lsum, tg, false, 0, grad_rec_tiles(c.ntact, live));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
