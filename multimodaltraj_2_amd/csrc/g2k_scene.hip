@@ -172,8 +172,11 @@ __host__ inline SceneLayout scene_layout(const g2k_dims* d, int NP, bool grad) {
   // frames (M, tiles, gradient) than workgroup 1 — the modular split left it
   // ~10k cycles behind (kfold4 train, profiles/r12j_*).  One frame per
   // producer measured best: kfold4 train 41.1 -> 38.6 us per step at 8 of 20
-  // frames, 42.0-42.2 at 7 or 9 (profiles/r12kl_*)
-  if (grad && l.split == 2 && !l.dwo_seq) l.own0 = NP;
+  // frames, 42.0-42.2 at 7 or 9 (profiles/r12kl_*).  With dWo added in frame
+  // order (Nmax > 85: many tiles per frame, the heads a small share) one
+  // frame fewer than half: dense_crowd train 105.0 -> 101.3 us at 9 of 20
+  // (8: 107.8, profiles/r12r_*, r12s_*)
+  if (grad && l.split == 2 && !nll) l.own0 = l.dwo_seq ? (fc / 2 - 1 > 1 ? fc / 2 - 1 : 1) : NP;
   return l;
 }
 
@@ -1422,7 +1425,7 @@ __device__ __forceinline__ void balance_stores(const StepArgs& a) {
 // REP (frames_invariant): frame f0 stands for the `nrep` frames fb .. fb +
 // nrep - 1 — its predictions are stored for each of them, its terms enter the
 // sums with weight nrep.
-template <bool PM, bool NLL, bool REP = false>
+template <bool PM, bool NLL, bool REP = false, bool BLK = false>
 __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout& lay,
                                             const SceneCtx& c, int slot, int fb, int f0, int fstep,
                                             int fend, unsigned act_bits, float (&acc)[5],
@@ -1439,7 +1442,15 @@ __device__ __forceinline__ void grad_frames(const StepArgs& a, const SceneLayout
   f32x4 dm[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   for (int fl = f0; fl < fend; fl += fstep) {
     const int f = fb + fl;
-    const int ford = f / lay.split;                      // the workgroup's own frames in order (dwo_seq)
+    // the workgroup's own frames in order (dwo_seq): modular ownership f /
+    // split; BLK: the own frames of the earlier (full) chunks, then the
+    // ordinal in this chunk's block
+    int ford = f / lay.split;
+    if (BLK) {
+      const int cnt = (c.nf - fb) < lay.fc ? (c.nf - fb) : lay.fc;
+      const int nfull = own_block0(lay.fc, lay.own0), n0 = own_block0(cnt, lay.own0);
+      ford = (fb / lay.fc) * (c.x == 0 ? nfull : lay.fc - nfull) + (c.x == 0 ? fl : fl - n0);
+    }
     poll_flag(c.sMflag + fl, f + 1);                     // M of this frame (a producer's head)
     const brsrc pr = REP ? make_brsrc(a.pred ? a.pred + ((size_t)c.s * F + fb) * kL2 * Nmax : a.targets,
                                       a.pred ? (uint32_t)(nrep * kL2 * Nmax * 4) : 0u)
@@ -1676,11 +1687,11 @@ __device__ __forceinline__ void scene_producer(const StepArgs& a, const SceneLay
     // phase 2 — predictions and errors (GRAD: and the gradient)
     if (CR) __builtin_amdgcn_s_setprio(3);
     if (GRAD) {
-      grad_frames<PM, NLL, INV>(a, lay, c, pw, fb, own.fo + (BLK ? 1 : c.X) * pw, (BLK ? 1 : c.X) * NP, own.fo + (BLK ? 1 : c.X) * gend,
+      grad_frames<PM, NLL, INV, BLK>(a, lay, c, pw, fb, own.fo + (BLK ? 1 : c.X) * pw, (BLK ? 1 : c.X) * NP, own.fo + (BLK ? 1 : c.X) * gend,
                                 act_bits, acc, lsum, tg[0], true, 0, -1, INV ? cnt : 1);
       if (pw < R && grad_rec_tiles(ntact, live) < ntact) {    // the recurrence waves' frames' other tiles
         const int fl = own.fo + (BLK ? 1 : c.X) * (gend + pw);
-        grad_frames<PM, NLL>(a, lay, c, pw, fb, fl, 1, fl + 1, act_bits, acc, lsum, tg[0], false,
+        grad_frames<PM, NLL, false, BLK>(a, lay, c, pw, fb, fl, 1, fl + 1, act_bits, acc, lsum, tg[0], false,
                              grad_rec_tiles(ntact, live), ntact);
       }
       // every worker done with the chunk's frames -> its dU rows into dV
@@ -1866,7 +1877,7 @@ __device__ __forceinline__ void rec_grad_work(const StepArgs& a, const SceneLayo
     const int R = INV ? 0 : grad_rec_frames(own.n, NP, live);   // (INV: producer 0 has the one frame)
     if (R > 0) {
       float2 tg[4];
-      grad_frames<PM, NLL>(a, lay, c, NP + c.wv, fb, own.fo + (BLK ? 1 : c.X) * (own.n - R + c.wv), (BLK ? 1 : c.X) * R,
+      grad_frames<PM, NLL, false, BLK>(a, lay, c, NP + c.wv, fb, own.fo + (BLK ? 1 : c.X) * (own.n - R + c.wv), (BLK ? 1 : c.X) * R,
                            own.fo + (BLK ? 1 : c.X) * own.n,
                            scene_act_bits(c, scene_mask_word(a, lay, c)),
                            acc, lsum, tg, false, 0, grad_rec_tiles(c.ntact, live));
