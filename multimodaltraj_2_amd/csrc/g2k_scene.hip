@@ -1357,9 +1357,10 @@ __device__ __forceinline__ unsigned scene_act_bits(const SceneCtx& c, uint32_t w
 // share shrinks when they have at least two frames each.
 __device__ __forceinline__ int grad_rec_frames(int cnt, int NP, bool live) {
   // a workgroup without the chain (a split scene's other workgroups): its
-  // recurrence waves are free from the start — whole frames, one each, once
-  // the producers keep one each
-  if (!live) return cnt >= NP + kRecW ? kRecW : 0;
+  // recurrence waves are free from the start — whole frames, one each, the
+  // frames past one per producer (dense_crowd's 11 of 20: 101.2 -> 99.8 us
+  // per train step, profiles/r12v_*)
+  if (!live) return cnt > NP ? (cnt - NP < kRecW ? cnt - NP : kRecW) : 0;
   return cnt >= 2 * NP ? kRecW : 0;
 }
 // ... split by tile when a frame has two or more: the recurrence wave takes
